@@ -1,0 +1,210 @@
+"""bench.py -- device-resident encode+repair throughput of the MI355X codec.
+
+One "step" = encode every object of the batch into all n = k+m replicas
+(chunk_generator<uint16_t>::write for replicas 0..n-1, chunk.h:245-281) and
+then repair every object from the k replicas left after erasing m of them
+(chunk_restore<uint16_t>::restore, chunk.h:290-444).  Inputs are synthetic
+(splitmix64) and already resident in HBM when timing starts.
+
+Default workload (BASELINE.json configs[1]/[2]): k=16, m=4, 1024 objects of
+64 MiB per GPU, erasures {0,5,10,15}.  Multi-GPU: one process per GPU
+(torchrun), objects round-robin by rank, no data-path collective ("weak"
+scaling: per-GPU work is fixed).  rank 0 prints ONE JSON line.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--k 16] [--m 4]
+                  [--objects 1024] [--object-mib 64] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SEED = 0x7664730000000000
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--k", type=int, default=16)
+    p.add_argument("--m", type=int, default=4)
+    p.add_argument("--objects", type=int, default=1024, help="objects per GPU")
+    p.add_argument("--object-mib", type=float, default=64.0)
+    p.add_argument("--erase", type=str, default="", help="comma list of erased replica ids")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-objects", type=int, default=3, help="objects in the CPU baseline sample")
+    return p.parse_args()
+
+
+def relaunch_with_torchrun(args) -> int:
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", "--master-port=29533", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_baseline(k, n, size, nodes, count):
+    """The oracle (CPU restatement of kernel/vds_data, single thread) timed on
+    a bounded sample of the same workload.  Test infrastructure: never part of
+    the GPU measurement."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ctypes as O
+    import numpy as np
+
+    O.lib()
+    objs = [O.splitmix(SEED + o, size) for o in range(count)]
+    t0 = time.perf_counter()
+    for d in objs:
+        chunks = [O.encode(k, r, d) for r in range(n)]
+        out = O.restore(k, nodes, [chunks[r] for r in nodes])
+        assert out is not None and out.size == size
+    dt = time.perf_counter() - t0
+    return {"value": round(count * size / dt / 2**30, 6), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{count} x {size >> 20} MiB objects, encode all {n} replicas + repair from {len(nodes)} "
+                      f"(oracle/vds_oracle.c, 1 thread, {dt:.2f} s)",
+            "seconds": round(dt, 3)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world == 1:
+        sys.exit(relaunch_with_torchrun(args))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    from vds_amd import build as vbuild
+    vbuild.build()
+    from vds_amd import chunk
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    k, m = args.k, args.m
+    n = k + m
+    size = int(args.object_mib * (1 << 20))
+    L = chunk.replica_size(k, size)
+    if args.erase:
+        erased = [int(x) for x in args.erase.split(",")]
+    else:
+        step = max(1, n // m)
+        erased = list(range(0, n, step))[:m]
+    nodes = [r for r in range(n) if r not in erased][:k]
+
+    # ---- memory plan: inputs + all replicas + restored objects, resident in HBM
+    objects = args.objects
+    free, _total = torch.cuda.mem_get_info(dev)
+    per_obj = size + n * L + size
+    if objects * per_obj > 0.92 * free:
+        objects = max(1, int(0.92 * free // per_obj))
+    inp = torch.empty(objects * size, dtype=torch.uint8, device=dev)
+    reps = torch.empty((n, objects * L), dtype=torch.uint8, device=dev)
+    restored = torch.empty(objects * size, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    for i in range(objects):  # object o = rank + world * i (round-robin ownership)
+        chunk.fill_splitmix_device(inp[i * size:], size, SEED + rank + world * i)
+    torch.cuda.synchronize(dev)
+
+    rep_ptrs = [reps[i].data_ptr() for i in range(n)]
+    chunk_ptrs = [reps[r].data_ptr() for r in nodes]
+    padding = size % (2 * k)
+
+    def encode():
+        chunk.encode_device(k, list(range(n)), inp, size, size, objects, rep_ptrs, L)
+
+    def repair():
+        chunk.restore_device(k, nodes, chunk_ptrs, L, L, padding, objects, restored, size)
+
+    for _ in range(args.warmup):
+        encode()
+        repair()
+    torch.cuda.synchronize(dev)
+    # correctness guard on the measured buffers (outside the timed region)
+    assert torch.equal(restored[:size], inp[:size]) and torch.equal(restored[-size:], inp[-size:]), \
+        "repair output differs from the input"
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        ev[s][0].record(stream)
+        encode()
+        ev[s][1].record(stream)
+        repair()
+        ev[s][2].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    enc_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps
+    rep_ms = sum(b.elapsed_time(c) for _, b, c in ev) / args.steps
+
+    if world > 1:
+        t = torch.tensor([elapsed, enc_ms, rep_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, enc_ms, rep_ms = (float(x) for x in t.tolist())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    total_bytes = world * objects * size
+    value = total_bytes / (elapsed / args.steps) / 2**30
+
+    enc_bytes = objects * (size + n * L)      # S + n*(2*ceil(S/2k)+2)
+    rep_bytes = objects * (k * L + size)      # k*L + S
+    if enc_ms >= rep_ms:
+        dom, dom_bytes, dom_ms = "k_encode_bs<16,20,5>" if (k, n) == (16, 20) else "k_encode_bs", enc_bytes, enc_ms
+    else:
+        dom, dom_bytes, dom_ms = "k_restore_bs<16>" if k == 16 else "k_restore_bs", rep_bytes, rep_ms
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+
+    result = {
+        "metric": "device-resident encode+repair GiB/s, k=16 m=4 64 MiB stripes, 1/2/4/8 GPU",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (splitmix64 objects generated on device)",
+        "config": {"workload": f"k={k},m={m} encode of all {n} replicas + repair from {len(nodes)} "
+                               f"(erased {erased}), {objects} x {size >> 20} MiB objects per GPU",
+                   "k": k, "m": m, "objects_per_gpu": objects, "object_bytes": size,
+                   "erased": erased, "parallelism": f"objects round-robin over {world} GPU(s), no collective"},
+        "encode_GiBps": round(world * objects * size / (enc_ms * 1e-3) / 2**30, 3),
+        "repair_GiBps": round(world * objects * size / (rep_ms * 1e-3) / 2**30, 3),
+        "encode_ms": round(enc_ms, 3),
+        "repair_ms": round(rep_ms, 3),
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(k, n, size, nodes, args.cpu_objects)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

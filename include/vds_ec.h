@@ -1,0 +1,150 @@
+/*
+ * vds_ec.h -- C ABI of the MI355X-native object-chunk erasure codec.
+ *
+ * This is the boundary that replaces the CPU arithmetic of lboss75/vds
+ * kernel/vds_data (chunk.h, gf.h, chunk_storage.cpp).  The reference's codec
+ * is header-only C++ templates; the drop-in headers in vds_amd/include/vds_data/
+ * keep that exact template API and forward the uint8_t / uint16_t
+ * instantiations to the entry points below (see INTEGRATION.md for the
+ * binding).  Plain pointers, sizes and int status codes only.
+ *
+ * Terminology (reference): an object of S bytes is cut into stripes of
+ * k cells; a "replica" (horcrux) with id r holds, per stripe, the evaluation
+ * at r of the polynomial whose coefficients are the stripe's cells
+ * (chunk.h:245-281), followed by a 2-byte big-endian trailer S mod (k*cell).
+ * Any k distinct replicas restore the object (chunk.h:290-444).
+ *
+ * Memory: *_device entry points take device pointers and enqueue work on the
+ * given hipStream_t (NULL = the per-thread default stream) without
+ * synchronising.  *_host entry points take host pointers, stage through
+ * pinned buffers on the current device and return when the result is in host
+ * memory.  Every entry point fails with VDS_EC_ENODEV if no GPU is usable --
+ * there is no CPU fallback.
+ */
+#ifndef VDS_EC_H_
+#define VDS_EC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ----------------------------------------------------------- status codes */
+#define VDS_EC_OK 0
+#define VDS_EC_EINVAL (-1)    /* bad argument (k == 0, null pointer, size)     */
+#define VDS_EC_ENODEV (-2)    /* no usable GPU / HIP runtime error at init    */
+#define VDS_EC_ENOMEM (-3)    /* device or pinned allocation failed           */
+#define VDS_EC_ESINGULAR (-4) /* replica ids not distinct: V not invertible   */
+#define VDS_EC_ERESTORE (-5)  /* "Fatal error at chunk_restore::restore"      */
+#define VDS_EC_EHIP (-6)      /* HIP runtime error during a launch / copy     */
+
+/* ----------------------------------------------------------------- flags */
+/* write_padding = false in chunk_generator::write (chunk.h:79,273-278):
+ * no trailer; the caller guarantees size % (k*cell) == 0.                  */
+#define VDS_EC_F_NO_TRAILER 0x1u
+/* Cell-array form (test path, chunk.h:206-224 and chunk.h:383-400): data is
+ * an array of native-endian cells, no trailer, restore is not trimmed.     */
+#define VDS_EC_F_CELLS 0x2u
+
+#define VDS_EC_MAX_K 65535u
+
+const char *vds_ec_strerror(int status);
+int vds_ec_version(void);
+/* Number of HIP devices usable by the library (0 on a machine with none). */
+int vds_ec_device_count(int *count);
+
+/* Bytes chunk_generator<cell>::write appends for one replica
+ * (chunk.h:248 expected_size + chunk.h:274 trailer).  cell_bytes = 1 | 2. */
+uint64_t vds_ec_replica_size(unsigned cell_bytes, unsigned k, uint64_t size, unsigned flags);
+/* Bytes chunk_restore<cell>::restore returns for replicas of replica_size
+ * bytes with trailer `padding` (chunk.h:415-419).                           */
+uint64_t vds_ec_restored_size(unsigned cell_bytes, unsigned k, uint64_t replica_size, uint16_t padding);
+
+/* ---------------------------------------------------- field / matrix helpers
+ * Replace gf_math<uint16_t>() / gf_math<uint8_t>() (gf.h:131-253),
+ * chunk<cell>::generate_multipliers (chunk.h:183-194) and the
+ * chunk_restore<cell> constructor (chunk.h:290-375).  Host-only, no GPU.   */
+int vds_ec_gf16_tables(uint16_t *value2log, uint16_t *log2value); /* 65536 each */
+int vds_ec_gf8_tables(uint8_t *value2log, uint8_t *log2value);    /* 256 each   */
+int vds_ec_multipliers16(uint16_t k, uint16_t node, uint16_t *out);
+int vds_ec_multipliers8(uint8_t k, uint8_t node, uint8_t *out);
+/* out = V^{-1} (k*k, row-major) for V[i][c] = nodes[i]^c.  Returns
+ * VDS_EC_ESINGULAR when two nodes coincide (the reference computes garbage
+ * there: its validation is vds_assert, compiled out).        */
+int vds_ec_inverse16(uint16_t k, const uint16_t *nodes, uint16_t *out);
+int vds_ec_inverse8(uint8_t k, const uint8_t *nodes, uint8_t *out);
+
+/* -------------------------------------------------------- device entry points
+ * Encode `count` objects of `size` bytes each: object o at in + o*in_stride.
+ * For each of the n replica ids, replica r_i of object o is written at
+ * outs[i] + o*out_stride (outs is a HOST array of n device pointers) and
+ * occupies vds_ec_replica_size(...) bytes.  Replaces n calls of
+ * chunk_generator<uint16_t>(k, r_i).write(s, data, size) per object
+ * (chunk.h:245-281; caller loops dht_network_client.cpp:75-77, :589-591).  */
+int vds_ec_encode16_device(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *in,
+                           uint64_t size, uint64_t in_stride, uint32_t count, uint8_t *const *outs,
+                           uint64_t out_stride, unsigned flags, void *stream);
+int vds_ec_encode8_device(uint8_t k, const uint8_t *replicas, uint32_t n, const uint8_t *in,
+                          uint64_t size, uint64_t in_stride, uint32_t count, uint8_t *const *outs,
+                          uint64_t out_stride, unsigned flags, void *stream);
+
+/* Restore `count` objects from k replicas each: replica j (id nodes[j]) of
+ * object o at chunks[j] + o*chunk_stride (chunks: HOST array of k device
+ * pointers), chunk_size bytes each (trailer included).  The restored object
+ * o is written at out + o*out_stride; its size (identical for all objects,
+ * taken from the trailer of object 0's first chunk ON THE HOST -- so the
+ * caller passes it in `padding`) is vds_ec_restored_size(...).  Replaces
+ * chunk_restore<uint16_t>(k, nodes).restore(chunks) (chunk.h:290-444;
+ * caller dht_network_client.cpp:887-888).                                   */
+int vds_ec_restore16_device(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks,
+                            uint64_t chunk_size, uint64_t chunk_stride, uint16_t padding,
+                            uint32_t count, uint8_t *out, uint64_t out_stride, unsigned flags,
+                            void *stream);
+int vds_ec_restore8_device(uint8_t k, const uint8_t *nodes, const uint8_t *const *chunks,
+                           uint64_t chunk_size, uint64_t chunk_stride, uint16_t padding,
+                           uint32_t count, uint8_t *out, uint64_t out_stride, unsigned flags,
+                           void *stream);
+
+/* ---------------------------------------------------------- host entry points
+ * Same operations on host memory (pinned staging, H2D -> kernel -> D2H on
+ * the calling thread's current device).  outs: n host buffers of
+ * vds_ec_replica_size(...) bytes.  This is what chunk_generator::write and
+ * chunk_storage::generate_replica (chunk_storage.cpp:41-60) call.            */
+int vds_ec_encode16_host(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data,
+                         uint64_t size, uint8_t *const *outs, unsigned flags);
+int vds_ec_encode8_host(uint8_t k, const uint8_t *replicas, uint32_t n, const uint8_t *data,
+                        uint64_t size, uint8_t *const *outs, unsigned flags);
+/* chunks: k host buffers of chunk_size bytes; out must hold
+ * (chunk_size-2)*k bytes (chunk_size*k for VDS_EC_F_CELLS); *out_size
+ * receives the restored length (chunk.h:402-444, chunk_storage.cpp:62-86). */
+int vds_ec_restore16_host(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks,
+                          uint64_t chunk_size, uint8_t *out, uint64_t *out_size, unsigned flags);
+int vds_ec_restore8_host(uint8_t k, const uint8_t *nodes, const uint8_t *const *chunks,
+                         uint64_t chunk_size, uint8_t *out, uint64_t *out_size, unsigned flags);
+
+/* Batched host-memory encode across every visible GPU (one host thread,
+ * pinned ring and stream pair per device; object o -> device o % devices).
+ * objs[o] has sizes[o] bytes; replica i of object o goes to outs[o*n + i].
+ * This is the save_temp / save_data formulation.    */
+int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
+                               const uint8_t *const *objs, const uint64_t *sizes, uint32_t count,
+                               uint8_t *const *outs, unsigned flags, int max_devices);
+
+/* ----------------------------------------------------------------- utilities */
+/* Fill `size` device bytes at dst with the splitmix64 stream of `seed`
+ * (little-endian 8-byte words) -- the synthetic-object generator used by
+ * bench.py and the parity tests (SURVEY.md 8(c) "Input PRNG").               */
+int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void *stream);
+
+/* Which kernel path a device call with these parameters takes: 2 = bit-sliced
+ * fast path for the full tiles (+ generic tail), 1 = generic path only.     */
+int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint64_t size);
+int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VDS_EC_H_ */

@@ -1,0 +1,351 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle.
+
+Bit-exact for every byte (integer/byte arithmetic: no tolerance).  Covers
+the bit-sliced fast kernels (k=16/n=20, k=32/n=40, k=4/n=6 with contiguous
+replica ids and >= one 2048-stripe tile) and the generic kernels (every other
+shape, the tails, the trailers), both cell widths, the cell-array test paths,
+the reference's own round-trip tests re-hosted, and full BASELINE sizes via
+frozen oracle SHA-256s and round-trip properties.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+with open(os.path.join(GOLDEN, "golden_vectors.json")) as _f:
+    G = json.load(_f)
+SEED = G["seed_base"]
+
+
+def sha(a) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def ec(gpu):
+    import vds_amd
+    return vds_amd
+
+
+# ------------------------------------------------------------------ helpers
+
+def dev_object(torch, size, index):
+    from vds_amd import chunk
+    t = torch.empty(max(size, 1), dtype=torch.uint8, device="cuda")
+    chunk.fill_splitmix_device(t, size, SEED + index)
+    return t
+
+
+def dev_encode(torch, k, n, t, size, count=1, stride=None, replicas=None):
+    """Encode `count` objects laid out at `stride` in t; returns [count][n] uint8 tensors."""
+    from vds_amd import chunk
+    replicas = list(range(n)) if replicas is None else replicas
+    L = chunk.replica_size(k, size)
+    stride = size if stride is None else stride
+    out = torch.zeros((len(replicas), count, max(L, 1)), dtype=torch.uint8, device="cuda")
+    ptrs = [out[i].data_ptr() for i in range(len(replicas))]
+    chunk.encode_device(k, replicas, t, size, stride, count, ptrs, out.shape[2])
+    torch.cuda.synchronize()
+    return out[:, :, :L]
+
+
+# ------------------------------------------------------------------- inputs
+
+def test_fill_splitmix_matches_oracle(ec):
+    import torch
+    for size, idx in ((0, 0), (1, 1), (7, 2), (8, 3), (1000, 4), (1 << 20, 5)):
+        t = dev_object(torch, size, idx)
+        assert t[:size].cpu().numpy().tobytes() == O.splitmix(SEED + idx, size).tobytes()
+
+
+# ------------------------------------------------------------------- encode
+
+def test_encode_small_golden_host_api(ec):
+    for e in G["encode16_small"]:
+        d = O.splitmix(SEED + e["object_index"], e["size"])
+        outs = ec.chunk.encode_host(e["k"], list(range(6)), d)
+        for r, hexs in e["replicas"].items():
+            assert outs[int(r)].tobytes().hex() == hexs
+        for r in range(6):  # per-replica drop-in call (chunk_generator::write)
+            assert ec.ChunkGenerator(e["k"], r).write(d).tobytes().hex() == e["replicas"][str(r)]
+
+
+@pytest.mark.parametrize("entry", G["encode16_sha"], ids=lambda e: f"k{e['k']}n{e['n']}s{e['size']}")
+def test_encode_golden_sha(ec, entry):
+    import torch
+    k, n, size = entry["k"], entry["n"], entry["size"]
+    t = dev_object(torch, size, entry["object_index"])
+    out = dev_encode(torch, k, n, t, size)
+    for r in range(n):
+        assert sha(out[r, 0].cpu().numpy()) == entry["sha256"][str(r)], f"replica {r}"
+    if "head64" in entry:
+        for r in range(n):
+            assert out[r, 0, :64].cpu().numpy().tobytes().hex() == entry["head64"][str(r)]
+
+
+def test_encode_special_inputs(ec):
+    for e in G["encode16_special"]:
+        d = np.full(e["size"], e["fill"], dtype=np.uint8)
+        outs = ec.chunk.encode_host(e["k"], list(range(e["n"])), d)
+        for r in range(e["n"]):
+            assert sha(outs[r]) == e["sha256"][str(r)]
+
+
+def test_encode_random_shapes_vs_oracle(ec):
+    rng = np.random.default_rng(11)
+    for trial in range(40):
+        k = int(rng.integers(1, 41))
+        size = int(rng.choice([0, 1, 2, 3, int(rng.integers(1, 5000)), int(rng.integers(5000, 300000))]))
+        n = int(rng.integers(1, 9))
+        ids = [int(x) for x in rng.choice(70000 if trial % 2 else 64, n, replace=False) % 65536]
+        d = rng.integers(0, 256, size, dtype=np.uint8)
+        outs = ec.chunk.encode_host(k, ids, d)
+        for i, r in enumerate(ids):
+            assert np.array_equal(outs[i], O.encode(k, r, d)), (k, size, r)
+        nopad = ec.chunk.encode_host(k, ids[:1], d, write_padding=False)[0]
+        assert np.array_equal(nopad, O.encode(k, ids[0], d, write_padding=False))
+
+
+@pytest.mark.parametrize("k,n", [(16, 20), (32, 40), (4, 6)])
+def test_fast_encode_tiles_and_tail_vs_oracle(ec, k, n):
+    """>= 1 bit-sliced tile plus a ragged tail and a partial last stripe."""
+    import torch
+    from vds_amd import _lib
+    tile_bytes = 2048 * 2 * k
+    for size in (tile_bytes, tile_bytes + 1, 3 * tile_bytes + 2 * k * 5 + 3):
+        assert _lib.lib().vds_ec_encode16_path(k, (np.arange(n, dtype=np.uint16)).ctypes.data_as(_lib.u16p),
+                                               n, size) == 2
+        t = dev_object(torch, size, 1000 + size % 97)
+        d = t[:size].cpu().numpy()
+        out = dev_encode(torch, k, n, t, size)
+        for r in range(n):
+            assert np.array_equal(out[r, 0].cpu().numpy(), O.encode(k, r, d)), (k, size, r)
+
+
+def test_fast_equals_generic_path(ec):
+    import torch
+    k, n, size = 16, 20, 5 * 65536 + 123
+    t = dev_object(torch, size, 77)
+    fast = dev_encode(torch, k, n, t, size)
+    perm = list(range(n))[::-1]  # non-contiguous ids -> generic kernel
+    gen = dev_encode(torch, k, n, t, size, replicas=perm)
+    for i, r in enumerate(perm):
+        assert torch.equal(fast[r], gen[i])
+
+
+def test_batched_objects_with_strides(ec):
+    import torch
+    k, n, size, count = 16, 20, 2 * 65536 + 1000, 5
+    stride = size + 4096
+    t = torch.empty(stride * count, dtype=torch.uint8, device="cuda")
+    from vds_amd import chunk
+    for o in range(count):
+        chunk.fill_splitmix_device(t[o * stride:], size, SEED + 500 + o)
+    out = dev_encode(torch, k, n, t, size, count=count, stride=stride)
+    for o in range(count):
+        d = O.splitmix(SEED + 500 + o, size)
+        for r in (0, 1, 7, 19):
+            assert np.array_equal(out[r, o].cpu().numpy(), O.encode(k, r, d))
+
+
+# ------------------------------------------------------------------ restore
+
+@pytest.mark.parametrize("entry", G["restore16"], ids=lambda e: f"k{e['k']}s{e['size']}")
+def test_restore_golden(ec, entry):
+    k, size = entry["k"], entry["size"]
+    d = O.splitmix(SEED + entry["object_index"], size)
+    chunks = [O.encode(k, r, d) for r in entry["nodes"]]
+    out = ec.ChunkRestore(k, entry["nodes"]).restore(chunks)
+    assert sha(out) == entry["sha256"]
+    assert out.tobytes() == d.tobytes()
+
+
+def test_restore_random_vs_oracle(ec):
+    rng = np.random.default_rng(5)
+    for trial in range(30):
+        k = int(rng.integers(1, 35))
+        size = int(rng.choice([0, 1, 2, int(rng.integers(1, 3000)), int(rng.integers(3000, 200000))]))
+        d = rng.integers(0, 256, size, dtype=np.uint8)
+        nodes = [int(x) for x in rng.choice(65536 if trial % 3 == 0 else 80, k, replace=False)]
+        chunks = [O.encode(k, r, d) for r in nodes]
+        out = ec.ChunkRestore(k, nodes).restore(chunks)
+        ref = O.restore(k, nodes, chunks)
+        assert ref is not None and np.array_equal(out, ref), (k, size)
+
+
+@pytest.mark.parametrize("k,n", [(16, 20), (32, 40)])
+def test_fast_restore_tiles_and_tail(ec, k, n):
+    import torch
+    from vds_amd import chunk, _lib
+    tile_bytes = 2048 * 2 * k
+    for size in (tile_bytes, 2 * tile_bytes + 2 * k * 3 + 1):
+        t = dev_object(torch, size, 2000 + size % 89)
+        enc = dev_encode(torch, k, n, t, size)
+        for erased in ([0, 1, 2, 3][: n - k], list(range(n - (n - k), n)), list(range(0, n, n // (n - k)))[: n - k]):
+            nodes = [r for r in range(n) if r not in erased][:k]
+            L = enc.shape[2]
+            assert _lib.lib().vds_ec_restore16_path(k, None, L) == 2
+            out = torch.zeros(size + 64, dtype=torch.uint8, device="cuda")
+            chunk.restore_device(k, nodes, [enc[r, 0].data_ptr() for r in nodes], L, 0, size % (2 * k), 1, out, 0)
+            torch.cuda.synchronize()
+            assert torch.equal(out[:size], t[:size]), (size, erased)
+            assert int(out[size:].sum().item()) == 0  # trimmed to E bytes
+
+
+def test_restore_device_batched(ec):
+    import torch
+    from vds_amd import chunk
+    k, n, size, count = 16, 20, 65536 * 3 + 17, 3
+    t = torch.empty(size * count, dtype=torch.uint8, device="cuda")
+    for o in range(count):
+        chunk.fill_splitmix_device(t[o * size:], size, SEED + 900 + o)
+    enc = dev_encode(torch, k, n, t, size, count=count)
+    nodes = [r for r in range(n) if r not in (0, 5, 10, 15)]
+    L = enc.shape[2]
+    out = torch.zeros(size * count, dtype=torch.uint8, device="cuda")
+    # chunk j of object o at enc[nodes[j], o]: stride between objects = L
+    chunk.restore_device(k, nodes, [enc[r, 0].data_ptr() for r in nodes], L, enc.stride(1), size % (2 * k),
+                         count, out, size)
+    torch.cuda.synchronize()
+    assert torch.equal(out, t)
+
+
+def test_restore_error_paths(ec):
+    from vds_amd import VdsEcError
+    d = O.splitmix(SEED + 3, 100)
+    chunks = [O.encode(4, r, d) for r in (1, 2, 3, 4)]
+    with pytest.raises(VdsEcError):  # duplicate replica ids
+        ec.ChunkRestore(4, [1, 2, 2, 4]).restore(chunks)
+    bad = [c.copy() for c in chunks]
+    for c in bad:  # trailer claims more bytes than the chunks can produce
+        c[-2:] = [0xFF, 0xFF]
+    assert O.restore(4, [1, 2, 3, 4], bad) is None
+    with pytest.raises(VdsEcError):
+        ec.ChunkRestore(4, [1, 2, 3, 4]).restore(bad)
+    # a trailer that is wrong but within range decodes the trailer row like the reference
+    odd = [c.copy() for c in chunks]
+    for c in odd:
+        c[-2:] = [0, 7]
+    ref = O.restore(4, [1, 2, 3, 4], odd)
+    assert ref is not None
+    assert np.array_equal(ec.ChunkRestore(4, [1, 2, 3, 4]).restore(odd), ref)
+
+
+# ----------------------------------------------------------- uint8_t / cells
+
+def test_uint8_instantiation(ec):
+    e = G["encode8"]
+    d = O.splitmix(SEED + e["object_index"], e["size"])
+    for r, h in e["replicas"].items():
+        assert sha(ec.ChunkGenerator(e["k"], int(r), cell_bytes=1).write(d)) == h
+    rng = np.random.default_rng(9)
+    for trial in range(20):
+        k = int(rng.integers(1, 30))
+        size = int(rng.integers(0, 20000))
+        d = rng.integers(0, 256, size, dtype=np.uint8)
+        nodes = [int(x) for x in rng.choice(256, k, replace=False)]
+        chunks = ec.chunk.encode_host(k, nodes, d, cell_bytes=1)
+        for i, r in enumerate(nodes):
+            assert np.array_equal(chunks[i], O.encode(k, r, d, cell_bytes=1))
+        out = ec.ChunkRestore(k, nodes, cell_bytes=1).restore(chunks)
+        assert np.array_equal(out, O.restore(k, nodes, chunks, cell_bytes=1))
+        assert out.tobytes() == d.tobytes()
+
+
+def test_cell_array_paths(ec):
+    c = G["chunk_cells16"]
+    cells = O.splitmix(SEED + c["object_index"], 2 * c["cells"]).view(np.uint16)
+    ids = [5, 9, 200]
+    got = {}
+    for r in ids:
+        got[r] = ec.chunk_cells(ec.ChunkGenerator(3, r), cells)
+        assert got[r].tolist() == c["chunks"][str(r)]
+    rest = ec.ChunkRestore(3, ids).restore_cells([got[r] for r in ids])
+    assert rest.tolist() == c["restore"]
+
+
+# ------------------------------------------- reference tests, re-hosted on GPU
+
+def test_chunk_tests_test_chunks_uint8(ec):
+    """chunk_tests.cpp:10-59 (seeded instead of time-seeded)."""
+    rng = np.random.default_rng(10)
+    for _ in range(10):
+        size = int(rng.integers(1, 1001))
+        size -= size % 3
+        data = rng.integers(0, 256, size, dtype=np.uint8)
+        ids = [int(x) for x in rng.choice(256, 3, replace=False)]
+        chunks = [ec.chunk_cells(ec.ChunkGenerator(3, r, cell_bytes=1), data) for r in ids]
+        res = ec.ChunkRestore(3, ids, cell_bytes=1).restore_cells(chunks)
+        assert res.size == size and np.array_equal(res, data)
+
+
+def test_chunk_tests_test_chunks16(ec):
+    """chunk_tests.cpp:61-110."""
+    rng = np.random.default_rng(11)
+    for _ in range(10):
+        size = int(rng.integers(1, 1001))
+        size -= size % 3
+        data = rng.integers(0, 65536, size).astype(np.uint16)
+        ids = [int(x) for x in rng.choice(256, 3, replace=False)]
+        chunks = [ec.chunk_cells(ec.ChunkGenerator(3, r), data) for r in ids]
+        res = ec.ChunkRestore(3, ids).restore_cells(chunks)
+        assert res.size == size and np.array_equal(res, data)
+
+
+def test_chunk_tests_test_chunks_storage(ec):
+    """chunk_tests.cpp:112-162: 800 distinct replicas < 1000, 2000-6000 bytes."""
+    rng = np.random.default_rng(12)
+    size = int(rng.integers(2000, 6001))
+    data = rng.integers(0, 256, size, dtype=np.uint8)
+    storage = ec.ChunkStorage(800)
+    ids = [int(x) for x in rng.choice(1000, 800, replace=False)]
+    horcruxes = {r: storage.generate_replica(r, data) for r in ids[:40]}
+    batch = storage.generate_replicas(ids[40:], data)
+    horcruxes.update({r: b for r, b in zip(ids[40:], batch)})
+    for r in ids[:3]:
+        assert np.array_equal(horcruxes[r], O.encode(800, r, data))
+    result = storage.restore_data(horcruxes)
+    assert result.size == size and result.tobytes() == data.tobytes()
+    from vds_amd import VdsEcError
+    with pytest.raises(VdsEcError):
+        storage.restore_data(dict(list(horcruxes.items())[:799]))  # "Error at restoring data"
+
+
+# ------------------------------------------------ full BASELINE-size properties
+
+@pytest.mark.parametrize("k,n", [(16, 20), (32, 40)])
+def test_full_size_roundtrip_64MiB(ec, k, n):
+    import torch
+    from vds_amd import chunk
+    size = 64 << 20
+    t = dev_object(torch, size, 0)
+    enc = dev_encode(torch, k, n, t, size)
+    L = enc.shape[2]
+    m = n - k
+    for erased in (list(range(m)), list(range(0, n, n // m))[:m], list(range(n - m, n))):
+        nodes = [r for r in range(n) if r not in erased]
+        out = torch.empty(size, dtype=torch.uint8, device="cuda")
+        chunk.restore_device(k, nodes, [enc[r, 0].data_ptr() for r in nodes], L, 0, size % (2 * k), 1, out, 0)
+        torch.cuda.synchronize()
+        assert torch.equal(out, t), erased
+    # linearity: enc(a ^ b) == enc(a) ^ enc(b) on the data cells
+    t2 = dev_object(torch, size, 1)
+    enc2 = dev_encode(torch, k, n, t2, size)
+    enc3 = dev_encode(torch, k, n, t ^ t2, size)
+    assert torch.equal(enc3[:, :, : L - 2], enc[:, :, : L - 2] ^ enc2[:, :, : L - 2])
+
+
+def test_host_batch_multi_device(ec):
+    rng = np.random.default_rng(13)
+    objs = [rng.integers(0, 256, int(s), dtype=np.uint8) for s in (0, 17, 65536 * 2 + 5, 300000, 4096)]
+    outs = ec.encode_host_batch(16, list(range(20)), objs)
+    for o, d in zip(outs, objs):
+        for r in (0, 3, 19):
+            assert np.array_equal(o[r], O.encode(16, r, d))

@@ -1,0 +1,258 @@
+"""Python mirror of lboss75/vds kernel/vds_data's chunk-transform API.
+
+Same names, argument meaning and error behaviour as the reference's C++
+templates (chunk.h:59-114, chunk_storage.h:13-34), backed by the HIP kernels
+through the C ABI.  `cell_bytes` selects the uint16_t (2, production) or
+uint8_t (1) instantiation.
+
+  ChunkGenerator(k, n).write(data, write_padding=True)   chunk.h:245-281
+  ChunkGenerator.write_padding(size)                     chunk.h:283-287
+  chunk_cells(generator, cells)                          chunk.h:206-224
+  ChunkRestore(k, nodes).restore(chunks)                 chunk.h:290-444
+  ChunkRestore.restore_cells(chunks)                     chunk.h:383-400
+  ChunkStorage(min_horcrux).generate_replica / restore_data
+                                                         chunk_storage.cpp:41-86
+  encode_device / restore_device                          batched device-memory
+                                                         forms for torch tensors
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Iterable, Mapping, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import F_CELLS, F_NO_TRAILER, VdsEcError, check
+
+__all__ = [
+    "ChunkGenerator", "ChunkRestore", "ChunkStorage", "chunk_cells", "replica_size",
+    "encode_device", "restore_device", "fill_splitmix_device", "encode_host_batch",
+    "VdsEcError", "multipliers", "inverse",
+]
+
+
+def _u8(data) -> np.ndarray:
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(data), dtype=np.uint8)
+    return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+
+
+def _ids(values: Iterable[int], cell_bytes: int) -> np.ndarray:
+    dt = np.uint16 if cell_bytes == 2 else np.uint8
+    return np.ascontiguousarray(np.asarray(list(values), dtype=np.int64).astype(dt))
+
+
+def _idp(a: np.ndarray, cell_bytes: int):
+    return a.ctypes.data_as(_lib.u16p if cell_bytes == 2 else _lib.u8p)
+
+
+def replica_size(k: int, size: int, cell_bytes: int = 2, write_padding: bool = True) -> int:
+    return int(_lib.lib().vds_ec_replica_size(cell_bytes, k, size, 0 if write_padding else F_NO_TRAILER))
+
+
+def multipliers(k: int, node: int, cell_bytes: int = 2) -> np.ndarray:
+    """chunk<cell>::generate_multipliers (chunk.h:183-194)."""
+    dt = np.uint16 if cell_bytes == 2 else np.uint8
+    out = np.zeros(k, dtype=dt)
+    f = _lib.lib().vds_ec_multipliers16 if cell_bytes == 2 else _lib.lib().vds_ec_multipliers8
+    check(f(k, node, _idp(out, cell_bytes)))
+    return out
+
+
+def inverse(k: int, nodes: Sequence[int], cell_bytes: int = 2) -> np.ndarray:
+    """The chunk_restore<cell>(k, n) multipliers matrix (chunk.h:290-375)."""
+    ids = _ids(nodes, cell_bytes)
+    dt = np.uint16 if cell_bytes == 2 else np.uint8
+    out = np.zeros(k * k, dtype=dt)
+    f = _lib.lib().vds_ec_inverse16 if cell_bytes == 2 else _lib.lib().vds_ec_inverse8
+    check(f(k, _idp(ids, cell_bytes), _idp(out, cell_bytes)), "chunk_restore")
+    return out.reshape(k, k)
+
+
+class ChunkGenerator:
+    """chunk_generator<cell>(k, n) (chunk.h:59-88, 232-243)."""
+
+    def __init__(self, k: int, n: int, cell_bytes: int = 2):
+        if cell_bytes not in (1, 2):
+            raise ValueError("cell_bytes must be 1 (uint8_t) or 2 (uint16_t)")
+        limit = 0xFFFF if cell_bytes == 2 else 0xFF
+        self._k = int(k) & limit  # cell_type arithmetic
+        self._n = int(n) & limit
+        self.cell_bytes = cell_bytes
+        self._mult = multipliers(self._k, self._n, cell_bytes)
+
+    def k(self) -> int:
+        return self._k
+
+    def n(self) -> int:
+        return self._n
+
+    def multipliers(self) -> np.ndarray:
+        return self._mult
+
+    def write(self, data, write_padding: bool = True) -> np.ndarray:
+        """Bytes chunk_generator::write appends to the serializer."""
+        return encode_host(self._k, [self._n], data, self.cell_bytes, write_padding)[0]
+
+    def write_padding(self, size: int) -> np.ndarray:
+        pad = size % (self.cell_bytes * self._k)  # chunk.h:286
+        return np.array([(pad >> 8) & 0xFF, pad & 0xFF], dtype=np.uint8)
+
+
+def encode_host(k: int, replicas: Sequence[int], data, cell_bytes: int = 2,
+                write_padding: bool = True, cells: bool = False) -> list:
+    """All requested replicas of one host object in one device pass."""
+    buf = _u8(data)
+    ids = _ids(replicas, cell_bytes)
+    flags = (0 if write_padding else F_NO_TRAILER) | (F_CELLS if cells else 0)
+    L = int(_lib.lib().vds_ec_replica_size(cell_bytes, k, buf.size, flags))
+    outs = [np.empty(max(L, 1), dtype=np.uint8) for _ in range(ids.size)]
+    ptrs = (C.c_void_p * max(1, ids.size))(*[o.ctypes.data for o in outs])
+    f = _lib.lib().vds_ec_encode16_host if cell_bytes == 2 else _lib.lib().vds_ec_encode8_host
+    check(f(k, _idp(ids, cell_bytes), ids.size, buf.ctypes.data if buf.size else None, buf.size, ptrs, flags),
+          "chunk_generator::write")
+    return [o[:L] for o in outs]
+
+
+def chunk_cells(generator: ChunkGenerator, cells) -> np.ndarray:
+    """chunk<cell>(generator, data, len).data() (chunk.h:206-224)."""
+    dt = np.uint16 if generator.cell_bytes == 2 else np.uint8
+    arr = np.ascontiguousarray(cells, dtype=dt)
+    out = encode_host(generator.k(), [generator.n()], arr.view(np.uint8), generator.cell_bytes, cells=True)[0]
+    return out.view(dt).copy()
+
+
+class ChunkRestore:
+    """chunk_restore<cell>(k, n) (chunk.h:90-114, 290-444)."""
+
+    def __init__(self, k: int, nodes: Sequence[int], cell_bytes: int = 2):
+        self._k = int(k)
+        self.cell_bytes = cell_bytes
+        self._nodes = _ids(nodes, cell_bytes)
+        if self._nodes.size < self._k:
+            raise ValueError("chunk_restore needs k replica ids")
+        self._nodes = self._nodes[: self._k]
+        self._error = None
+        try:
+            self._mult = inverse(self._k, self._nodes, cell_bytes)
+        except VdsEcError as e:  # duplicate ids: the reference yields garbage here
+            self._mult = None
+            self._error = e
+
+    def multipliers(self) -> np.ndarray:
+        if self._error is not None:
+            raise self._error
+        return self._mult
+
+    def restore(self, chunks: Sequence) -> np.ndarray:
+        """chunk_restore::restore(const std::vector<const_data_buffer>&)."""
+        if self._error is not None:
+            raise self._error
+        bufs = [_u8(c) for c in chunks[: self._k]]
+        if len(bufs) < self._k:
+            raise VdsEcError(_lib.EINVAL, "chunk_restore::restore")
+        size = bufs[0].size
+        if any(b.size != size for b in bufs):
+            raise VdsEcError(_lib.EINVAL, "chunk_restore::restore")
+        out = np.empty(max(1, (size - 2) * self._k if size >= 2 else 1), dtype=np.uint8)
+        out_size = C.c_uint64(0)
+        ptrs = (C.c_void_p * self._k)(*[b.ctypes.data for b in bufs])
+        f = _lib.lib().vds_ec_restore16_host if self.cell_bytes == 2 else _lib.lib().vds_ec_restore8_host
+        check(f(self._k, _idp(self._nodes, self.cell_bytes), ptrs, size, out.ctypes.data, C.byref(out_size), 0),
+              "chunk_restore::restore")
+        return out[: out_size.value]
+
+    def restore_cells(self, chunks: Sequence) -> np.ndarray:
+        """chunk_restore::restore(std::vector<cell>&, const chunk<cell>**)."""
+        if self._error is not None:
+            raise self._error
+        dt = np.uint16 if self.cell_bytes == 2 else np.uint8
+        arrs = [np.ascontiguousarray(c, dtype=dt) for c in chunks[: self._k]]
+        n_cells = arrs[0].size
+        out = np.empty(max(1, n_cells * self._k), dtype=dt)
+        out_size = C.c_uint64(0)
+        ptrs = (C.c_void_p * self._k)(*[a.ctypes.data for a in arrs])
+        f = _lib.lib().vds_ec_restore16_host if self.cell_bytes == 2 else _lib.lib().vds_ec_restore8_host
+        check(f(self._k, _idp(self._nodes, self.cell_bytes), ptrs, n_cells * self.cell_bytes, out.ctypes.data,
+                C.byref(out_size), F_CELLS), "chunk_restore::restore")
+        return out[: n_cells * self._k]
+
+
+class ChunkStorage:
+    """chunk_storage (chunk_storage.h:13-34, chunk_storage.cpp:10-86)."""
+
+    def __init__(self, min_horcrux: int):
+        self.min_horcrux = int(min_horcrux) & 0xFFFF
+        self._generators: Dict[int, ChunkGenerator] = {}
+
+    def generate_replica(self, replica: int, data) -> np.ndarray:
+        g = self._generators.get(replica)
+        if g is None:
+            g = self._generators[replica] = ChunkGenerator(self.min_horcrux, replica)
+        return g.write(data)
+
+    def generate_replicas(self, replicas: Sequence[int], data) -> list:
+        """Batched form of generate_replica for the save_temp / save_data loops."""
+        return encode_host(self.min_horcrux, replicas, data)
+
+    def restore_data(self, horcruxes: Mapping[int, object]) -> np.ndarray:
+        if self.min_horcrux != len(horcruxes):
+            raise VdsEcError(_lib.EINVAL, "Error at restoring data")  # chunk_storage.cpp:65-67
+        items = list(horcruxes.items())
+        size = _u8(items[0][1]).size
+        for _, v in items:
+            if _u8(v).size != size:
+                raise VdsEcError(_lib.EINVAL, "Error at restoring data")  # chunk_storage.cpp:76-78
+        return ChunkRestore(self.min_horcrux, [r for r, _ in items]).restore([v for _, v in items])
+
+
+# --------------------------------------------------------------- device forms
+
+def _stream_ptr(stream) -> int | None:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return int(stream)
+
+
+def encode_device(k: int, replicas: Sequence[int], inp, size: int, in_stride: int, count: int,
+                  outs: Sequence[int], out_stride: int, write_padding: bool = True, stream=None) -> None:
+    """vds_ec_encode16_device on raw device pointers (ints) / torch tensors."""
+    ids = _ids(replicas, 2)
+    ptrs = (C.c_void_p * ids.size)(*[int(o) for o in outs])
+    in_ptr = inp.data_ptr() if hasattr(inp, "data_ptr") else int(inp)
+    check(_lib.lib().vds_ec_encode16_device(k, _idp(ids, 2), ids.size, in_ptr, size, in_stride, count, ptrs,
+                                            out_stride, 0 if write_padding else F_NO_TRAILER,
+                                            _stream_ptr(stream)), "encode16_device")
+
+
+def restore_device(k: int, nodes: Sequence[int], chunks: Sequence[int], chunk_size: int, chunk_stride: int,
+                   padding: int, count: int, out, out_stride: int, stream=None) -> None:
+    ids = _ids(nodes, 2)
+    ptrs = (C.c_void_p * ids.size)(*[int(c) for c in chunks])
+    out_ptr = out.data_ptr() if hasattr(out, "data_ptr") else int(out)
+    check(_lib.lib().vds_ec_restore16_device(k, _idp(ids, 2), ptrs, chunk_size, chunk_stride, padding, count,
+                                             out_ptr, out_stride, 0, _stream_ptr(stream)), "restore16_device")
+
+
+def fill_splitmix_device(dst, size: int, seed: int, stream=None) -> None:
+    ptr = dst.data_ptr() if hasattr(dst, "data_ptr") else int(dst)
+    check(_lib.lib().vds_ec_fill_splitmix_device(ptr, size, seed, _stream_ptr(stream)), "fill_splitmix")
+
+
+def encode_host_batch(k: int, replicas: Sequence[int], objects: Sequence, max_devices: int = 0) -> list:
+    """Multi-GPU host-memory encode (one thread + pinned ring per device)."""
+    ids = _ids(replicas, 2)
+    bufs = [_u8(o) for o in objects]
+    sizes = np.array([b.size for b in bufs], dtype=np.uint64)
+    outs = []
+    for b in bufs:
+        L = replica_size(k, b.size)
+        outs.append([np.empty(max(L, 1), dtype=np.uint8) for _ in range(ids.size)])
+    optrs = (C.c_void_p * (len(bufs) * ids.size))(*[o.ctypes.data for row in outs for o in row])
+    iptrs = (C.c_void_p * max(1, len(bufs)))(*[b.ctypes.data for b in bufs])
+    check(_lib.lib().vds_ec_encode16_host_batch(k, _idp(ids, 2), ids.size, iptrs,
+                                                sizes.ctypes.data_as(_lib.u64p), len(bufs), optrs, 0,
+                                                max_devices), "encode16_host_batch")
+    return [[o[: replica_size(k, b.size)] for o in row] for row, b in zip(outs, bufs)]

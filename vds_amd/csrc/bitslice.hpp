@@ -1,0 +1,197 @@
+// bitslice.hpp -- bit-sliced GF(2^16) arithmetic on 32-stripe "planes".
+//
+// A Plane16 holds one GF(2^16) value for each of 32 independent stripes:
+// word p[b] carries bit b of the 32 values (bit position = stripe slot).
+// Field addition is a per-word XOR; multiplication by x is a rotation of the
+// word indices plus three XORs (x^16 = x^12 + x^3 + x + 1, gf.h:114-119);
+// multiplication by a compile-time constant C is Horner over the bits of C.
+// Because every index is a compile-time constant after unrolling, the
+// "rotation" is register renaming and costs nothing.
+//
+// The transposes convert between this layout and the byte layout of the
+// reference (big-endian 16-bit cells, binary_serialize.cpp:18-22).
+#pragma once
+
+#include "gf_common.hpp"
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define VDS_INLINE __host__ __device__ __forceinline__
+#else
+#define VDS_INLINE inline
+#endif
+
+namespace vds_ec {
+
+struct Plane16 {
+  uint32_t p[16];
+};
+
+VDS_INLINE Plane16 plane_xor(const Plane16 &a, const Plane16 &b) {
+  Plane16 r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r.p[i] = a.p[i] ^ b.p[i];
+  return r;
+}
+
+VDS_INLINE Plane16 plane_xor3(const Plane16 &a, const Plane16 &b, const Plane16 &c) {
+  Plane16 r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r.p[i] = a.p[i] ^ b.p[i] ^ c.p[i];
+  return r;
+}
+
+VDS_INLINE Plane16 plane_zero() {
+  Plane16 r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r.p[i] = 0;
+  return r;
+}
+
+// a * x  (mod x^16 + x^12 + x^3 + x + 1)
+VDS_INLINE Plane16 plane_mulx(const Plane16 &a) {
+  Plane16 r;
+  const uint32_t t = a.p[15];
+  r.p[0] = t;
+  r.p[1] = a.p[0] ^ t;
+  r.p[2] = a.p[1];
+  r.p[3] = a.p[2] ^ t;
+#pragma unroll
+  for (int i = 4; i < 12; ++i) r.p[i] = a.p[i - 1];
+  r.p[12] = a.p[11] ^ t;
+  r.p[13] = a.p[12];
+  r.p[14] = a.p[13];
+  r.p[15] = a.p[14];
+  return r;
+}
+
+// Horner over the bits of C below bit B+1: u <- u*x (+ a if bit set).
+template <uint32_t C, int B>
+struct PlaneMulC {
+  VDS_INLINE static Plane16 run(const Plane16 &u, const Plane16 &a) {
+    Plane16 v = plane_mulx(u);
+    if constexpr (((C >> B) & 1u) != 0) v = plane_xor(v, a);
+    return PlaneMulC<C, B - 1>::run(v, a);
+  }
+};
+template <uint32_t C>
+struct PlaneMulC<C, -1> {
+  VDS_INLINE static Plane16 run(const Plane16 &u, const Plane16 &) { return u; }
+};
+
+// a * C for a compile-time field constant C (< 2^16).
+template <uint32_t C>
+VDS_INLINE Plane16 plane_mulc(const Plane16 &a) {
+  if constexpr (C == 0) {
+    return plane_zero();
+  } else {
+    constexpr int top = poly_degree(C);
+    return PlaneMulC<C, top - 1>::run(a, a);
+  }
+}
+
+// Horner step of the encode: acc * C + x.
+template <uint32_t C>
+VDS_INLINE Plane16 plane_horner(const Plane16 &acc, const Plane16 &x) {
+  if constexpr (C == 0) {
+    return x;
+  } else {
+    constexpr int top = poly_degree(C);
+    if constexpr (top == 0) {
+      return plane_xor(acc, x);
+    } else {
+      // Bits top-1 .. 1 of C (== bits top-2 .. 0 of C>>1), then fuse the last
+      // "+acc" with "+x" so the compiler can form v_xor3_b32.
+      const Plane16 v = PlaneMulC<(C >> 1), top - 2>::run(acc, acc);
+      const Plane16 w = plane_mulx(v);
+      if constexpr ((C & 1u) != 0)
+        return plane_xor3(w, acc, x);
+      else
+        return plane_xor(w, x);
+    }
+  }
+}
+
+// Multiply by a wave-uniform runtime constant c (< 2^16): Horner over all 16
+// bit positions.  The x-shift is unconditional so its index rotation stays a
+// static register renaming; only the add is a (uniform) branch on c.
+VDS_INLINE Plane16 plane_mul_rt(const Plane16 &a, uint32_t c) {
+  Plane16 u = plane_zero();
+#pragma unroll
+  for (int b = 15; b >= 0; --b) {
+    u = plane_mulx(u);
+    if ((c >> b) & 1u) u = plane_xor(u, a);
+  }
+  return u;
+}
+
+// ---------------------------------------------------------------- transposes
+
+// One butterfly round of the bit transpose for a power-of-two shift J < 8:
+// swaps (row k, bits with J set) <-> (row k+J, bits with J clear).
+template <int J, int ROWS, typename Arr>
+VDS_INLINE void transpose_round(Arr &A) {
+  constexpr uint32_t m = (J == 4) ? 0x0F0F0F0Fu : (J == 2) ? 0x33333333u : 0x55555555u;
+#pragma unroll
+  for (int k0 = 0; k0 < ROWS; k0 += 2 * J)
+#pragma unroll
+    for (int k = k0; k < k0 + J; ++k) {
+      const uint32_t a = A[k], b = A[k + J];
+      A[k] = (a & m) | ((b << J) & ~m);
+      A[k + J] = ((a >> J) & m) | (b & ~m);
+    }
+}
+
+// 32x32 bit transpose in place: afterwards A[p] bit i == before A[i] bit p.
+VDS_INLINE void transpose32(uint32_t (&A)[32]) {
+  // j = 16: swap (row k, bits 16..31) <-> (row k+16, bits 0..15)
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t a = A[k], b = A[k + 16];
+#if defined(__HIP_DEVICE_COMPILE__)
+    A[k] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+    A[k + 16] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+#else
+    A[k] = (a & 0x0000FFFFu) | (b << 16);
+    A[k + 16] = (a >> 16) | (b & 0xFFFF0000u);
+#endif
+  }
+  // j = 8
+#pragma unroll
+  for (int k0 = 0; k0 < 32; k0 += 16)
+#pragma unroll
+    for (int k = k0; k < k0 + 8; ++k) {
+      const uint32_t a = A[k], b = A[k + 8];
+#if defined(__HIP_DEVICE_COMPILE__)
+      A[k] = __builtin_amdgcn_perm(b, a, 0x06020400u);
+      A[k + 8] = __builtin_amdgcn_perm(b, a, 0x07030501u);
+#else
+      A[k] = (a & 0x00FF00FFu) | ((b << 8) & 0xFF00FF00u);
+      A[k + 8] = ((a >> 8) & 0x00FF00FFu) | (b & 0xFF00FF00u);
+#endif
+    }
+  // j = 4, 2, 1 : bitfield inserts
+  transpose_round<4, 32>(A);
+  transpose_round<2, 32>(A);
+  transpose_round<1, 32>(A);
+}
+
+// Two independent 16x16 bit transposes held in the low / high halves of 16
+// words: afterwards A[q] bit (16h + j) == before A[j] bit (16h + q).
+VDS_INLINE void transpose16x2(uint32_t (&A)[16]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t a = A[k], b = A[k + 8];
+#if defined(__HIP_DEVICE_COMPILE__)
+    A[k] = __builtin_amdgcn_perm(b, a, 0x06020400u);
+    A[k + 8] = __builtin_amdgcn_perm(b, a, 0x07030501u);
+#else
+    A[k] = (a & 0x00FF00FFu) | ((b << 8) & 0xFF00FF00u);
+    A[k + 8] = ((a >> 8) & 0x00FF00FFu) | (b & 0xFF00FF00u);
+#endif
+  }
+  transpose_round<4, 16>(A);
+  transpose_round<2, 16>(A);
+  transpose_round<1, 16>(A);
+}
+
+}  // namespace vds_ec

@@ -1,0 +1,76 @@
+// ec_internal.hpp -- launch interface between the C ABI (vds_ec_api.cpp) and
+// the kernels (ec_kernels.hip).  Internal to libvds_ec.so.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+namespace vds_ec {
+
+constexpr int kMaxLaunchReplicas = 64;  // replicas per generic encode launch
+constexpr int kMaxFastK = 32;
+constexpr uint32_t kTileStripes = 2048;  // 64 lanes x 32 bit-sliced slots
+
+struct GenericEncodeArgs {
+  const uint8_t *in;
+  uint64_t size;       // object bytes (cell arrays: bytes too)
+  uint64_t in_stride;  // bytes between objects
+  uint32_t count;      // objects
+  uint32_t k;
+  uint32_t cell_bytes; // 1 or 2
+  uint32_t flags;
+  uint32_t nrep;
+  uint64_t t_begin;    // first stripe handled
+  uint64_t t_count;    // stripes handled (the trailer is one extra index)
+  uint64_t stripes;    // total stripes T of an object
+  uint32_t write_trailer;
+  uint64_t out_stride;
+  uint16_t nodes[kMaxLaunchReplicas];
+  uint8_t *outs[kMaxLaunchReplicas];
+};
+
+struct GenericRestoreArgs {
+  const uint8_t *const *chunks;  // device array of k pointers
+  const uint16_t *matrix;        // device k*k inverse (row-major)
+  uint64_t chunk_stride;
+  uint32_t count;
+  uint32_t k;
+  uint32_t cell_bytes;
+  uint32_t flags;
+  uint64_t t_begin;
+  uint64_t t_count;
+  uint8_t *out;
+  uint64_t out_stride;
+  uint64_t out_len;  // bytes of the restored object (trim bound)
+};
+
+struct FastEncodeArgs {
+  const uint8_t *in;
+  uint64_t in_stride;
+  uint64_t out_stride;
+  uint32_t tiles_per_obj;
+  uint32_t total_tiles;
+  uint8_t *outs[kMaxLaunchReplicas];  // outs[r] for replica id r = 0..N-1
+};
+
+struct FastRestoreArgs {
+  const uint8_t *chunks[kMaxFastK];
+  uint64_t chunk_stride;
+  uint8_t *out;
+  uint64_t out_stride;
+  uint32_t tiles_per_obj;
+  uint32_t total_tiles;
+  uint16_t matrix[kMaxFastK * kMaxFastK];
+};
+
+hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s);
+hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s);
+// Returns hipErrorNotSupported when no bit-sliced instantiation exists for (k, n).
+hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, hipStream_t s);
+bool has_encode_fast(uint32_t k, uint32_t n);
+hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t s);
+bool has_restore_fast(uint32_t k);
+hipError_t launch_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed, hipStream_t s);
+
+}  // namespace vds_ec

@@ -1,0 +1,497 @@
+// ec_kernels.hip -- CDNA4 (gfx950) kernels of the object-chunk erasure codec.
+//
+//  * k_encode_generic / k_restore_generic: any k, any replica ids, 8- or
+//    16-bit cells.  One lane per output cell, carry-less field multiply.
+//    These handle the tails of the fast kernels and every shape the fast
+//    kernels are not instantiated for.
+//  * k_encode_bs<K,N>: bit-sliced encode of replicas 0..N-1 for full tiles of
+//    2048 stripes (lane = set of 32 stripes, one bit per stripe in each
+//    32-bit plane).  The workgroup's waves split the input transposes, share
+//    the bit planes through LDS, and each wave evaluates a compile-time group
+//    of replicas by Horner with constant multipliers (chunk.h:245-281 is a
+//    polynomial evaluation at the replica id).
+//  * k_restore_bs<K>: bit-sliced restore with the k x k inverse as
+//    wave-uniform runtime constants (chunk.h:402-444).
+//  * k_fill_splitmix: synthetic objects on the device.
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <utility>
+
+#include "bitslice.hpp"
+#include "ec_internal.hpp"
+
+namespace vds_ec {
+
+// ============================================================ generic kernels
+
+template <int CB>
+__device__ __forceinline__ uint32_t gf_mul_cell(uint32_t a, uint32_t b) {
+  if constexpr (CB == 2)
+    return gf16_mul(a, b);
+  else
+    return gf8_mul(a, b);
+}
+
+// Cell j of stripe t of an object, zero beyond `size` (chunk.h:254-260).
+template <int CB>
+__device__ __forceinline__ uint32_t read_cell(const uint8_t *obj, uint64_t size, uint64_t t, uint32_t j,
+                                              uint32_t k, bool native) {
+  const uint64_t pos = (t * k + j) * CB;
+  if constexpr (CB == 1) {
+    return pos < size ? obj[pos] : 0u;
+  } else {
+    if (native) {  // cell arrays: whole native uint16 cells (chunk.h:213-221)
+      return pos + 1 < size ? (uint32_t)(obj[pos] | (obj[pos + 1] << 8)) : 0u;
+    }
+    uint32_t hi = pos < size ? obj[pos] : 0u;
+    uint32_t lo = pos + 1 < size ? obj[pos + 1] : 0u;
+    return (hi << 8) | lo;
+  }
+}
+
+template <int CB>
+__global__ void k_encode_generic(GenericEncodeArgs a) {
+  const uint64_t per_rep = a.t_count + (a.write_trailer ? 1 : 0);
+  const uint64_t total = per_rep * a.nrep * (uint64_t)a.count;
+  const bool native = (a.flags & 0x2u) != 0;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t ti = idx % per_rep;
+    const uint64_t rest = idx / per_rep;
+    const uint32_t i = (uint32_t)(rest % a.nrep);
+    const uint32_t o = (uint32_t)(rest / a.nrep);
+    uint8_t *out = a.outs[i] + (uint64_t)o * a.out_stride;
+    if (ti == a.t_count) {
+      // trailer BE16(size % (k*cell)) after the T cells (chunk.h:273-275)
+      const uint64_t pad = a.size % ((uint64_t)a.k * CB);
+      out[a.stripes * CB] = (uint8_t)(pad >> 8);
+      out[a.stripes * CB + 1] = (uint8_t)(pad & 0xFF);
+      continue;
+    }
+    const uint64_t t = a.t_begin + ti;
+    const uint8_t *obj = a.in + (uint64_t)o * a.in_stride;
+    const uint32_t node = a.nodes[i];
+    uint32_t acc = 0;
+    for (int32_t j = (int32_t)a.k - 1; j >= 0; --j)  // Horner: sum_j node^j x_j
+      acc = gf_mul_cell<CB>(acc, node) ^ read_cell<CB>(obj, a.size, t, (uint32_t)j, a.k, native);
+    if constexpr (CB == 2) {
+      if (native) {
+        out[2 * t] = (uint8_t)(acc & 0xFF);
+        out[2 * t + 1] = (uint8_t)(acc >> 8);
+      } else {
+        out[2 * t] = (uint8_t)(acc >> 8);  // binary_serialize.cpp:18-22
+        out[2 * t + 1] = (uint8_t)(acc & 0xFF);
+      }
+    } else {
+      out[t] = (uint8_t)acc;
+    }
+  }
+}
+
+template <int CB>
+__global__ void k_restore_generic(GenericRestoreArgs a) {
+  const uint64_t per_obj = a.t_count * a.k;
+  const uint64_t total = per_obj * a.count;
+  const bool native = (a.flags & 0x2u) != 0;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t o = (uint32_t)(idx / per_obj);
+    const uint64_t r = idx % per_obj;
+    const uint64_t t = a.t_begin + r / a.k;
+    const uint32_t m = (uint32_t)(r % a.k);
+    const uint64_t pos = (t * a.k + m) * CB;
+    if (pos >= a.out_len) continue;
+    uint32_t acc = 0;
+    const uint16_t *row = a.matrix + (uint64_t)m * a.k;
+    for (uint32_t j = 0; j < a.k; ++j) {
+      const uint8_t *c = a.chunks[j] + (uint64_t)o * a.chunk_stride + t * CB;
+      uint32_t cell;
+      if constexpr (CB == 2)
+        cell = native ? (uint32_t)(c[0] | (c[1] << 8)) : (uint32_t)((c[0] << 8) | c[1]);
+      else
+        cell = c[0];
+      acc ^= gf_mul_cell<CB>(row[j], cell);
+    }
+    uint8_t *out = a.out + (uint64_t)o * a.out_stride;
+    if constexpr (CB == 2) {
+      const uint8_t b0 = native ? (uint8_t)(acc & 0xFF) : (uint8_t)(acc >> 8);
+      const uint8_t b1 = native ? (uint8_t)(acc >> 8) : (uint8_t)(acc & 0xFF);
+      out[pos] = b0;
+      if (pos + 1 < a.out_len) out[pos + 1] = b1;  // trimmed to E bytes (chunk.h:437-439)
+    } else {
+      out[pos] = (uint8_t)acc;
+    }
+  }
+}
+
+// ========================================================== bit-sliced encode
+
+constexpr int popcount32(uint32_t v) {
+  int c = 0;
+  for (int i = 0; i < 32; ++i) c += (v >> i) & 1u;
+  return c;
+}
+
+// Relative VALU cost of one Horner step for replica r (3 XOR per x-shift,
+// 16 per add): used to balance replicas across waves.
+constexpr int horner_cost(int r) { return r == 0 ? 1 : 3 * poly_degree((uint32_t)r) + 16 * popcount32((uint32_t)r); }
+
+template <int N, int WAVES, int RPW>
+struct ReplicaPlan {
+  int rep[WAVES][RPW];
+};
+
+// Longest-processing-time assignment of replicas 0..N-1 to waves.
+template <int N, int WAVES, int RPW>
+constexpr ReplicaPlan<N, WAVES, RPW> plan_replicas() {
+  ReplicaPlan<N, WAVES, RPW> p{};
+  int load[WAVES] = {};
+  int cnt[WAVES] = {};
+  bool used[N] = {};
+  for (int w = 0; w < WAVES; ++w)
+    for (int s = 0; s < RPW; ++s) p.rep[w][s] = -1;
+  for (int it = 0; it < N; ++it) {
+    int best = -1;
+    for (int r = 0; r < N; ++r)
+      if (!used[r] && (best < 0 || horner_cost(r) > horner_cost(best))) best = r;
+    used[best] = true;
+    int bw = -1;
+    for (int w = 0; w < WAVES; ++w)
+      if (cnt[w] < RPW && (bw < 0 || load[w] < load[bw])) bw = w;
+    p.rep[bw][cnt[bw]++] = best;
+    load[bw] += horner_cost(best);
+  }
+  return p;
+}
+
+template <int K, int N, int RPW>
+struct EncodeShape {
+  static constexpr int kWaves = (N + RPW - 1) / RPW;
+  static constexpr int kThreads = kWaves * 64;
+  static constexpr int kWordGroups = K / 2;                 // dwords per stripe
+  static constexpr int kGroupsPerWave = kWordGroups / kWaves;
+  static constexpr int kSetWords = K * 16 + 4;              // planes per set + pad
+  static constexpr int kLdsBytes = 64 * kSetWords * 4;
+  static constexpr ReplicaPlan<N, kWaves, RPW> kPlan = plan_replicas<N, kWaves, RPW>();
+  static_assert(kWordGroups % kWaves == 0, "word groups must split evenly over waves");
+  static_assert(K % 2 == 0, "fast path needs even k");
+};
+
+__device__ __forceinline__ Plane16 lds_planes(const uint32_t *p) {
+  Plane16 x;
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const uint4 v = q[m];
+    x.p[4 * m + 0] = v.x;
+    x.p[4 * m + 1] = v.y;
+    x.p[4 * m + 2] = v.z;
+    x.p[4 * m + 3] = v.w;
+  }
+  return x;
+}
+
+// Transpose one replica's planes back to big-endian cells and store them:
+// lane l pairs with lane l^1 so every store is a 4-byte word of two adjacent
+// stripes' cells.
+__device__ __forceinline__ void store_replica(const Plane16 &acc, uint8_t *base, uint32_t sel) {
+  uint32_t rows[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) rows[j] = acc.p[j ^ 8];  // word bit j <-> cell bit j^8 (BE)
+  transpose16x2(rows);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const uint32_t nb = (uint32_t)__shfl_xor((int)rows[q], 1);
+    *reinterpret_cast<uint32_t *>(base + 128 * q) = __builtin_amdgcn_perm(nb, rows[q], sel);
+  }
+}
+
+template <int K, int N, int RPW, int W>
+__device__ __forceinline__ void encode_wave_group(const uint32_t *set_planes, const FastEncodeArgs &a,
+                                                  uint64_t out_off, uint32_t sel) {
+  using S = EncodeShape<K, N, RPW>;
+  Plane16 acc[RPW];
+  {
+    const Plane16 x = lds_planes(set_planes + (K - 1) * 16);
+#pragma unroll
+    for (int s = 0; s < RPW; ++s) acc[s] = x;
+  }
+#pragma clang loop unroll(disable)
+  for (int c = K - 2; c >= 0; --c) {
+    const Plane16 x = lds_planes(set_planes + c * 16);
+    [&]<size_t... I>(std::index_sequence<I...>) {
+      ((S::kPlan.rep[W][I] >= 0
+            ? (void)(acc[I] = plane_horner<(uint32_t)(S::kPlan.rep[W][I] < 0 ? 0 : S::kPlan.rep[W][I])>(acc[I], x))
+            : (void)0),
+       ...);
+    }(std::make_index_sequence<RPW>{});
+  }
+#pragma unroll
+  for (int s = 0; s < RPW; ++s) {
+    const int r = S::kPlan.rep[W][s];
+    if (r >= 0) store_replica(acc[s], a.outs[r] + out_off, sel);
+  }
+}
+
+template <int K, int N, int RPW, int W>
+__device__ __forceinline__ void encode_dispatch(int wave, const uint32_t *set_planes, const FastEncodeArgs &a,
+                                                uint64_t out_off, uint32_t sel) {
+  using S = EncodeShape<K, N, RPW>;
+  if constexpr (W < S::kWaves) {
+    if (wave == W)
+      encode_wave_group<K, N, RPW, W>(set_planes, a, out_off, sel);
+    else
+      encode_dispatch<K, N, RPW, W + 1>(wave, set_planes, a, out_off, sel);
+  }
+}
+
+template <int K, int N, int RPW>
+__global__ __launch_bounds__((EncodeShape<K, N, RPW>::kThreads), 2) void k_encode_bs(FastEncodeArgs a) {
+  using S = EncodeShape<K, N, RPW>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t *my_set = lds + lane * S::kSetWords;
+  const uint32_t sel = (lane & 1) ? 0x03020706u : 0x05040100u;
+
+  for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+    const uint32_t o = tile / a.tiles_per_obj;
+    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
+    // ---- load this wave's word groups of the lane's 32 stripes
+    // slot i of lane l <-> stripe stripe0 + l + 64 i
+    const uint8_t *src = a.in + (uint64_t)o * a.in_stride + (stripe0 + lane) * (2 * K) +
+                         4 * (wave * S::kGroupsPerWave);
+    uint32_t R[S::kGroupsPerWave][32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const uint8_t *p = src + (uint64_t)i * 64 * (2 * K);
+      if constexpr (S::kGroupsPerWave == 2) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(p);
+        R[0][i] = v.x;
+        R[1][i] = v.y;
+      } else {
+#pragma unroll
+        for (int g = 0; g < S::kGroupsPerWave; ++g) R[g][i] = *reinterpret_cast<const uint32_t *>(p + 4 * g);
+      }
+    }
+    // ---- transpose to planes and publish in LDS: cell 2gw+h, bit b = R[g][16h + (b^8)]
+#pragma unroll
+    for (int g = 0; g < S::kGroupsPerWave; ++g) {
+      transpose32(R[g]);
+      const int gw = wave * S::kGroupsPerWave + g;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int b0 = 16 * h + 4 * (m ^ 2);
+          *reinterpret_cast<uint4 *>(my_set + (2 * gw + h) * 16 + 4 * m) =
+              make_uint4(R[g][b0], R[g][b0 + 1], R[g][b0 + 2], R[g][b0 + 3]);
+        }
+    }
+    __syncthreads();
+    // ---- evaluate this wave's replicas and store
+    const uint64_t out_off = (uint64_t)o * a.out_stride +
+                             2 * (stripe0 + ((lane & 1) ? (uint64_t)(lane - 1) + 1024 : (uint64_t)lane));
+    encode_dispatch<K, N, RPW, 0>(wave, my_set, a, out_off, sel);
+    __syncthreads();
+  }
+}
+
+// ========================================================= bit-sliced restore
+
+template <int K>
+struct RestoreShape {
+  static constexpr int kPerWave = 4;           // survivors loaded / outputs computed per wave
+  static constexpr int kWaves = K / kPerWave;
+  static constexpr int kThreads = 64 * kWaves;
+  static constexpr int kSetWords = K * 16 + 4;
+  static constexpr int kLdsBytes = 64 * kSetWords * 4;
+  static_assert(K % 8 == 0, "restore fast path needs k % 8 == 0");
+};
+
+// slot i (0..31) of lane l <-> stripe stripe0 + 8 l + 512 (i / 8) + (i % 8);
+// bit position pi of a plane <-> slot (pi < 16 ? 2 pi : 2 (pi - 16) + 1).
+__device__ __forceinline__ uint64_t restore_slot_stripe(int lane, int slot) {
+  return 8u * lane + 512u * (slot >> 3) + (slot & 7);
+}
+
+template <int K>
+__global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(FastRestoreArgs a) {
+  using S = RestoreShape<K>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t *my_set = lds + lane * S::kSetWords;
+
+  for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+    const uint32_t o = tile / a.tiles_per_obj;
+    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
+    // ---- load + transpose this wave's survivors
+#pragma unroll
+    for (int s = 0; s < S::kPerWave; ++s) {
+      const int j = wave * S::kPerWave + s;
+      const uint8_t *src = a.chunks[j] + (uint64_t)o * a.chunk_stride + 2 * stripe0 + 16 * lane;
+      uint32_t W[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(src + 1024 * q);
+        W[4 * q + 0] = v.x;
+        W[4 * q + 1] = v.y;
+        W[4 * q + 2] = v.z;
+        W[4 * q + 3] = v.w;
+      }
+      transpose16x2(W);  // W[x] = plane of cell bit x^8
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        *reinterpret_cast<uint4 *>(my_set + j * 16 + 4 * m) =
+            make_uint4(W[4 * (m ^ 2)], W[4 * (m ^ 2) + 1], W[4 * (m ^ 2) + 2], W[4 * (m ^ 2) + 3]);
+    }
+    __syncthreads();
+    // ---- outputs m = wave*kPerWave + s : sum_j M[m][j] * Y_j
+    Plane16 acc[S::kPerWave];
+#pragma unroll
+    for (int s = 0; s < S::kPerWave; ++s) acc[s] = plane_zero();
+#pragma clang loop unroll(disable)
+    for (int j = 0; j < K; ++j) {
+      const Plane16 y = lds_planes(my_set + j * 16);
+#pragma unroll
+      for (int s = 0; s < S::kPerWave; ++s) {
+        const uint32_t c = a.matrix[(wave * S::kPerWave + s) * K + j];
+        acc[s] = plane_xor(acc[s], plane_mul_rt(y, c));
+      }
+    }
+    // ---- back to big-endian cells: word group w' = cells (2w', 2w'+1)
+    uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
+#pragma unroll
+    for (int g = 0; g < S::kPerWave / 2; ++g) {
+      uint32_t rows[32];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) rows[16 * h + j] = acc[2 * g + h].p[j ^ 8];
+      transpose32(rows);
+      const int wg = (wave * S::kPerWave) / 2 + g;
+#pragma unroll
+      for (int pi = 0; pi < 32; ++pi) {
+        const int slot = pi < 16 ? 2 * pi : 2 * (pi - 16) + 1;
+        const uint64_t t = stripe0 + restore_slot_stripe(lane, slot);
+        *reinterpret_cast<uint32_t *>(dst + t * (2 * K) + 4 * wg) = rows[pi];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================== synthetic data
+
+__global__ void k_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed) {
+  const uint64_t words = (size + 7) / 8;
+  for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < words;
+       w += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t z = seed + (w + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    if (8 * w + 8 <= size) {
+      *reinterpret_cast<uint64_t *>(dst + 8 * w) = z;
+    } else {
+      for (uint64_t b = 0; 8 * w + b < size; ++b) dst[8 * w + b] = (uint8_t)(z >> (8 * b));
+    }
+  }
+}
+
+// =================================================================== launchers
+
+static int grid_for(uint64_t work, int block) {
+  uint64_t g = (work + block - 1) / block;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s) {
+  const uint64_t work = (a.t_count + (a.write_trailer ? 1 : 0)) * a.nrep * (uint64_t)a.count;
+  if (work == 0) return hipSuccess;
+  const int grid = grid_for(work, 256);
+  if (a.cell_bytes == 2)
+    hipLaunchKernelGGL(k_encode_generic<2>, dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_encode_generic<1>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s) {
+  const uint64_t work = a.t_count * a.k * (uint64_t)a.count;
+  if (work == 0) return hipSuccess;
+  const int grid = grid_for(work, 256);
+  if (a.cell_bytes == 2)
+    hipLaunchKernelGGL(k_restore_generic<2>, dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_restore_generic<1>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int K, int N, int RPW>
+static hipError_t launch_encode_bs(const FastEncodeArgs &a, hipStream_t s) {
+  using S = EncodeShape<K, N, RPW>;
+  static bool configured = false;
+  if (!configured) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_encode_bs<K, N, RPW>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, S::kLdsBytes);
+    if (e != hipSuccess) return e;
+    configured = true;
+  }
+  const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
+  int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
+  if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_encode_bs<K, N, RPW>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  return hipGetLastError();
+}
+
+bool has_encode_fast(uint32_t k, uint32_t n) {
+  return (k == 16 && n == 20) || (k == 32 && n == 40) || (k == 4 && n == 6);
+}
+
+hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, hipStream_t s) {
+  if (k == 16 && n == 20) return launch_encode_bs<16, 20, 5>(a, s);
+  if (k == 32 && n == 40) return launch_encode_bs<32, 40, 5>(a, s);
+  if (k == 4 && n == 6) return launch_encode_bs<4, 6, 3>(a, s);
+  return hipErrorNotSupported;
+}
+
+template <int K>
+static hipError_t launch_restore_bs_k(const FastRestoreArgs &a, hipStream_t s) {
+  using S = RestoreShape<K>;
+  static bool configured = false;
+  if (!configured) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_restore_bs<K>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, S::kLdsBytes);
+    if (e != hipSuccess) return e;
+    configured = true;
+  }
+  const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
+  int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
+  if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_restore_bs<K>, dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  return hipGetLastError();
+}
+
+bool has_restore_fast(uint32_t k) { return k == 16 || k == 32; }
+
+hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t s) {
+  if (k == 16) return launch_restore_bs_k<16>(a, s);
+  if (k == 32) return launch_restore_bs_k<32>(a, s);
+  return hipErrorNotSupported;
+}
+
+hipError_t launch_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed, hipStream_t s) {
+  if (size == 0) return hipSuccess;
+  const int grid = grid_for((size + 7) / 8, 256);
+  hipLaunchKernelGGL(k_fill_splitmix, dim3(grid), dim3(256), 0, s, dst, size, seed);
+  return hipGetLastError();
+}
+
+}  // namespace vds_ec

@@ -1,0 +1,657 @@
+// vds_ec_api.cpp -- the C ABI declared in include/vds_ec.h.
+//
+// Host-side runtime of the codec: argument validation mirroring the
+// reference's contracts (chunk.h, chunk_storage.cpp), the Vandermonde
+// inverse (the chunk_restore constructor), dispatch between the bit-sliced
+// and generic kernels, host-memory staging and the multi-GPU batch driver.
+// All data-path arithmetic runs in the HIP kernels of ec_kernels.hip; the
+// only host arithmetic is on k x k matrices and tables.
+#include "../../include/vds_ec.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "ec_internal.hpp"
+#include "gf_common.hpp"
+
+using namespace vds_ec;
+
+namespace {
+
+constexpr int kVersion = 100;  // 0.1.0
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+int hip_status(hipError_t e) {
+  if (e == hipSuccess) return VDS_EC_OK;
+  if (e == hipErrorOutOfMemory) return VDS_EC_ENOMEM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice || e == hipErrorInsufficientDriver)
+    return VDS_EC_ENODEV;
+  return VDS_EC_EHIP;
+}
+
+int device_ready() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return VDS_EC_ENODEV;
+  return VDS_EC_OK;
+}
+
+// ---------------------------------------------------------------- inverse
+// M = V^{-1} for V[i][c] = a_i^c, by Lagrange: column i of M holds the
+// coefficients of prod_{j!=i} (z - a_j) / (a_i - a_j).  V^{-1} is unique, so
+// this equals the reference's cross-multiplied Gauss-Jordan
+// (chunk.h:290-375) bit for bit whenever the nodes are distinct.
+template <typename Mul, typename Inv>
+int lagrange_inverse(uint32_t k, const uint32_t *a, uint16_t *out, Mul mul, Inv inv) {
+  std::vector<uint32_t> N(k + 1, 0), q(k);
+  N[0] = 1;
+  for (uint32_t j = 0; j < k; ++j) {  // N(z) = prod (z + a_j)
+    for (uint32_t d = j + 1; d > 0; --d) N[d] = N[d - 1] ^ mul(a[j], N[d]);
+    N[0] = mul(a[j], N[0]);
+  }
+  for (uint32_t i = 0; i < k; ++i) {
+    q[k - 1] = N[k];  // synthetic division by (z + a_i)
+    for (uint32_t m = k - 1; m > 0; --m) q[m - 1] = N[m] ^ mul(a[i], q[m]);
+    uint32_t d = 0;  // Q_i(a_i) = prod_{j != i} (a_i + a_j)
+    for (uint32_t m = k; m > 0; --m) d = mul(d, a[i]) ^ q[m - 1];
+    if (d == 0) return VDS_EC_ESINGULAR;
+    const uint32_t di = inv(d);
+    for (uint32_t m = 0; m < k; ++m) out[(size_t)m * k + i] = (uint16_t)mul(q[m], di);
+  }
+  return VDS_EC_OK;
+}
+
+int inverse16(uint32_t k, const uint16_t *nodes, uint16_t *out) {
+  std::vector<uint32_t> a(nodes, nodes + k);
+  return lagrange_inverse(
+      k, a.data(), out, [](uint32_t x, uint32_t y) { return (uint32_t)gf16_mul(x, y); },
+      [](uint32_t x) { return (uint32_t)gf16_inv(x); });
+}
+
+int inverse8(uint32_t k, const uint8_t *nodes, uint16_t *out) {
+  std::vector<uint32_t> a(nodes, nodes + k);
+  return lagrange_inverse(
+      k, a.data(), out, [](uint32_t x, uint32_t y) { return (uint32_t)gf8_mul(x, y); },
+      [](uint32_t x) { return (uint32_t)gf8_inv(x); });
+}
+
+// --------------------------------------------------------- device params
+// Small parameter blocks (pointer arrays, k*k matrices) uploaded with
+// stream-ordered allocations so device calls stay asynchronous.
+struct DeviceBlock {
+  void *ptr = nullptr;
+  hipStream_t stream = nullptr;
+  hipError_t upload(const void *host, size_t bytes, hipStream_t s) {
+    stream = s;
+    hipError_t e = hipMallocAsync(&ptr, bytes, s);
+    if (e != hipSuccess) return e;
+    return hipMemcpyAsync(ptr, host, bytes, hipMemcpyHostToDevice, s);
+  }
+  ~DeviceBlock() {
+    if (ptr) (void)hipFreeAsync(ptr, stream);
+  }
+};
+
+// ---------------------------------------------------------- encode core
+int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n, const uint8_t *in,
+                  uint64_t size, uint64_t in_stride, uint32_t count, uint8_t *const *outs,
+                  uint64_t out_stride, unsigned flags, hipStream_t s) {
+  if (k == 0 || (n > 0 && (!replicas || !outs)) || (count > 0 && size > 0 && !in)) return VDS_EC_EINVAL;
+  if (n == 0 || count == 0) return VDS_EC_OK;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!outs[i]) return VDS_EC_EINVAL;
+  int rc = device_ready();
+  if (rc) return rc;
+  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
+  const bool trailer = !(flags & (VDS_EC_F_NO_TRAILER | VDS_EC_F_CELLS));
+  const uint64_t stripe_bytes = (uint64_t)k * cb;
+  const uint64_t T = (size + stripe_bytes - 1) / stripe_bytes;
+
+  // Bit-sliced path: 16-bit byte-API cells, replicas exactly 0..n-1.
+  uint64_t fast_stripes = 0;
+  bool contiguous = true;
+  for (uint32_t i = 0; i < n; ++i) contiguous &= (replicas[i] == i);
+  if (cb == 2 && !cells && contiguous && has_encode_fast(k, n)) {
+    const uint64_t full = size / stripe_bytes;  // stripes with no zero padding
+    const uint64_t tiles = full / kTileStripes;
+    const uint64_t total = tiles * count;
+    if (tiles > 0 && total <= 0xFFFFFFFFull) {
+      FastEncodeArgs fa{};
+      fa.in = in;
+      fa.in_stride = in_stride;
+      fa.out_stride = out_stride;
+      fa.tiles_per_obj = (uint32_t)tiles;
+      fa.total_tiles = (uint32_t)total;
+      for (uint32_t i = 0; i < n; ++i) fa.outs[i] = outs[i];
+      hipError_t e = launch_encode_fast(k, n, fa, s);
+      if (e != hipSuccess) return hip_status(e);
+      fast_stripes = tiles * kTileStripes;
+    }
+  }
+  // Generic path for the rest (+ trailers), in launches of <= 64 replicas.
+  for (uint32_t base = 0; base < n; base += kMaxLaunchReplicas) {
+    GenericEncodeArgs ga{};
+    ga.in = in;
+    ga.size = size;
+    ga.in_stride = in_stride;
+    ga.count = count;
+    ga.k = k;
+    ga.cell_bytes = cb;
+    ga.flags = flags;
+    ga.nrep = (n - base) < (uint32_t)kMaxLaunchReplicas ? (n - base) : (uint32_t)kMaxLaunchReplicas;
+    ga.t_begin = fast_stripes;
+    ga.t_count = T - fast_stripes;
+    ga.stripes = T;
+    ga.write_trailer = trailer ? 1 : 0;
+    ga.out_stride = out_stride;
+    for (uint32_t i = 0; i < ga.nrep; ++i) {
+      ga.nodes[i] = replicas[base + i];
+      ga.outs[i] = outs[base + i];
+    }
+    hipError_t e = launch_encode_generic(ga, s);
+    if (e != hipSuccess) return hip_status(e);
+  }
+  return VDS_EC_OK;
+}
+
+// --------------------------------------------------------- restore core
+int restore_device(unsigned cb, uint32_t k, const uint16_t *matrix, const uint8_t *const *chunks,
+                   uint64_t chunk_size, uint64_t chunk_stride, uint64_t out_len, uint32_t count,
+                   uint8_t *out, uint64_t out_stride, unsigned flags, hipStream_t s) {
+  if (count == 0 || out_len == 0) return VDS_EC_OK;
+  int rc = device_ready();
+  if (rc) return rc;
+  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
+  // Every cell of a chunk, the trailer cell included: with a corrupt trailer
+  // the reference decodes that row too (chunk.h:421-441).
+  const uint64_t cells_per_chunk = chunk_size / cb;
+  (void)cells;
+  const uint64_t stripe_bytes = (uint64_t)k * cb;
+  uint64_t need = (out_len + stripe_bytes - 1) / stripe_bytes;  // stripes that produce output
+  if (need > cells_per_chunk) need = cells_per_chunk;
+
+  uint64_t fast_stripes = 0;
+  if (cb == 2 && !cells && has_restore_fast(k)) {
+    const uint64_t full = out_len / stripe_bytes;
+    const uint64_t tiles = full / kTileStripes;
+    const uint64_t total = tiles * count;
+    if (tiles > 0 && total <= 0xFFFFFFFFull) {
+      FastRestoreArgs fa{};
+      for (uint32_t j = 0; j < k; ++j) fa.chunks[j] = chunks[j];
+      fa.chunk_stride = chunk_stride;
+      fa.out = out;
+      fa.out_stride = out_stride;
+      fa.tiles_per_obj = (uint32_t)tiles;
+      fa.total_tiles = (uint32_t)total;
+      std::memcpy(fa.matrix, matrix, sizeof(uint16_t) * k * k);
+      hipError_t e = launch_restore_fast(k, fa, s);
+      if (e != hipSuccess) return hip_status(e);
+      fast_stripes = tiles * kTileStripes;
+    }
+  }
+  if (need > fast_stripes) {
+    DeviceBlock dptrs, dmat;
+    hipError_t e = dptrs.upload(chunks, sizeof(uint8_t *) * k, s);
+    if (e == hipSuccess) e = dmat.upload(matrix, sizeof(uint16_t) * (size_t)k * k, s);
+    if (e != hipSuccess) return hip_status(e);
+    GenericRestoreArgs ga{};
+    ga.chunks = static_cast<const uint8_t *const *>(dptrs.ptr);
+    ga.matrix = static_cast<const uint16_t *>(dmat.ptr);
+    ga.chunk_stride = chunk_stride;
+    ga.count = count;
+    ga.k = k;
+    ga.cell_bytes = cb;
+    ga.flags = flags;
+    ga.t_begin = fast_stripes;
+    ga.t_count = need - fast_stripes;
+    ga.out = out;
+    ga.out_stride = out_stride;
+    ga.out_len = out_len;
+    e = launch_restore_generic(ga, s);
+    if (e != hipSuccess) return hip_status(e);
+  }
+  return VDS_EC_OK;
+}
+
+uint64_t restored_len(unsigned cb, uint32_t k, uint64_t chunk_size, uint16_t padding, unsigned flags,
+                      bool *ok) {
+  *ok = true;
+  if (flags & VDS_EC_F_CELLS) return (chunk_size / cb) * k * cb;  // chunk.h:388-399, untrimmed
+  if (chunk_size < 2) {
+    *ok = false;
+    return 0;
+  }
+  // chunk.h:415-419 (size_t arithmetic; wraps exactly like the reference)
+  uint64_t e = (chunk_size - 2) * k;
+  if (padding != 0) {
+    e -= (uint64_t)k * cb;
+    e += padding;
+  }
+  // The reference's loop produces at most (chunk_size/cb)*k*cb bytes before
+  // reporting "Fatal error at chunk_restore::restore" (chunk.h:421-443).
+  const uint64_t produced = (chunk_size / cb) * k * cb;
+  if (e > produced) *ok = false;
+  return e;
+}
+
+// --------------------------------------------------------- host staging
+struct HostCtx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t *d_in = nullptr;
+  size_t d_in_cap = 0;
+  uint8_t *d_out = nullptr;
+  size_t d_out_cap = 0;
+  ~HostCtx() {
+    if (device >= 0) {
+      (void)hipSetDevice(device);
+      if (d_in) (void)hipFree(d_in);
+      if (d_out) (void)hipFree(d_out);
+      if (stream) (void)hipStreamDestroy(stream);
+    }
+  }
+  int ensure(size_t in_bytes, size_t out_bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return VDS_EC_ENODEV;
+    if (dev != device) {
+      this->~HostCtx();
+      new (this) HostCtx();
+      device = dev;
+      if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VDS_EC_ENODEV;
+    }
+    if (in_bytes > d_in_cap) {
+      if (d_in) (void)hipFree(d_in);
+      d_in = nullptr;
+      d_in_cap = 0;
+      if (hipMalloc(&d_in, in_bytes) != hipSuccess) return VDS_EC_ENOMEM;
+      d_in_cap = in_bytes;
+    }
+    if (out_bytes > d_out_cap) {
+      if (d_out) (void)hipFree(d_out);
+      d_out = nullptr;
+      d_out_cap = 0;
+      if (hipMalloc(&d_out, out_bytes) != hipSuccess) return VDS_EC_ENOMEM;
+      d_out_cap = out_bytes;
+    }
+    return VDS_EC_OK;
+  }
+};
+
+thread_local HostCtx g_host_ctx;
+
+int encode_host(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data,
+                uint64_t size, uint8_t *const *outs, unsigned flags) {
+  if (k == 0 || (n > 0 && (!replicas || !outs)) || (size > 0 && !data)) return VDS_EC_EINVAL;
+  int rc = device_ready();
+  if (rc) return rc;
+  if (n == 0) return VDS_EC_OK;
+  const uint64_t L = vds_ec_replica_size(cb, k, size, flags);
+  HostCtx &c = g_host_ctx;
+  rc = c.ensure(size ? size : 1, L * n ? L * n : 1);
+  if (rc) return rc;
+  hipError_t e = hipSuccess;
+  if (size) e = hipMemcpyAsync(c.d_in, data, size, hipMemcpyHostToDevice, c.stream);
+  if (e != hipSuccess) return hip_status(e);
+  std::vector<uint8_t *> douts(n);
+  for (uint32_t i = 0; i < n; ++i) douts[i] = c.d_out + (uint64_t)i * L;
+  rc = encode_device(cb, k, replicas, n, c.d_in, size, size, 1, douts.data(), 0, flags, c.stream);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < n && L; ++i) {
+    e = hipMemcpyAsync(outs[i], douts[i], L, hipMemcpyDeviceToHost, c.stream);
+    if (e != hipSuccess) return hip_status(e);
+  }
+  return hip_status(hipStreamSynchronize(c.stream));
+}
+
+int restore_host(unsigned cb, uint32_t k, const uint16_t *matrix, const uint8_t *const *chunks,
+                 uint64_t chunk_size, uint64_t out_len, uint8_t *out, unsigned flags) {
+  HostCtx &c = g_host_ctx;
+  const uint64_t in_bytes = chunk_size * k;
+  int rc = c.ensure(in_bytes ? in_bytes : 1, out_len ? out_len : 1);
+  if (rc) return rc;
+  std::vector<const uint8_t *> dchunks(k);
+  for (uint32_t j = 0; j < k; ++j) {
+    hipError_t e = hipMemcpyAsync(c.d_in + (uint64_t)j * chunk_size, chunks[j], chunk_size,
+                                  hipMemcpyHostToDevice, c.stream);
+    if (e != hipSuccess) return hip_status(e);
+    dchunks[j] = c.d_in + (uint64_t)j * chunk_size;
+  }
+  rc = restore_device(cb, k, matrix, dchunks.data(), chunk_size, 0, out_len, 1, c.d_out, 0, flags, c.stream);
+  if (rc) return rc;
+  if (out_len) {
+    hipError_t e = hipMemcpyAsync(out, c.d_out, out_len, hipMemcpyDeviceToHost, c.stream);
+    if (e != hipSuccess) return hip_status(e);
+  }
+  return hip_status(hipStreamSynchronize(c.stream));
+}
+
+template <typename Id>
+int check_restore_args(uint32_t k, const Id *nodes, const uint8_t *const *chunks, uint64_t chunk_size) {
+  if (k == 0 || !nodes || !chunks) return VDS_EC_EINVAL;
+  for (uint32_t j = 0; j < k; ++j)
+    if (!chunks[j] && chunk_size) return VDS_EC_EINVAL;
+  return VDS_EC_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+
+extern "C" {
+
+const char *vds_ec_strerror(int status) {
+  switch (status) {
+    case VDS_EC_OK: return "ok";
+    case VDS_EC_EINVAL: return "invalid argument";
+    case VDS_EC_ENODEV: return "no usable GPU (vds_ec has no CPU fallback)";
+    case VDS_EC_ENOMEM: return "device or pinned allocation failed";
+    case VDS_EC_ESINGULAR: return "replica ids are not distinct (singular Vandermonde matrix)";
+    case VDS_EC_ERESTORE: return "Fatal error at chunk_restore::restore";
+    case VDS_EC_EHIP: return "HIP runtime error";
+    default: return "unknown vds_ec status";
+  }
+}
+
+int vds_ec_version(void) { return kVersion; }
+
+int vds_ec_device_count(int *count) {
+  if (!count) return VDS_EC_EINVAL;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return VDS_EC_OK;
+}
+
+uint64_t vds_ec_replica_size(unsigned cell_bytes, unsigned k, uint64_t size, unsigned flags) {
+  if (k == 0 || (cell_bytes != 1 && cell_bytes != 2)) return 0;
+  const uint64_t stripe = (uint64_t)cell_bytes * k;
+  const uint64_t cells = (size + stripe - 1) / stripe;
+  const bool trailer = !(flags & (VDS_EC_F_NO_TRAILER | VDS_EC_F_CELLS));
+  return cells * cell_bytes + (trailer ? 2 : 0);
+}
+
+uint64_t vds_ec_restored_size(unsigned cell_bytes, unsigned k, uint64_t replica_size, uint16_t padding) {
+  bool ok = true;
+  uint64_t e = restored_len(cell_bytes, k, replica_size, padding, 0, &ok);
+  return ok ? e : 0;
+}
+
+int vds_ec_gf16_tables(uint16_t *value2log, uint16_t *log2value) {
+  if (!value2log || !log2value) return VDS_EC_EINVAL;
+  // gf.h:197-216: log2value[l] = x^l for l < 65535, value2log inverse,
+  // value2log[0] = 0 and log2value[65535] = 0 (never read).
+  std::memset(value2log, 0, 65536 * sizeof(uint16_t));
+  std::memset(log2value, 0, 65536 * sizeof(uint16_t));
+  uint32_t v = 1;
+  for (uint32_t l = 0; l < 65535; ++l) {
+    log2value[l] = (uint16_t)v;
+    value2log[v] = (uint16_t)l;
+    v = gf16_mul(v, 2);
+  }
+  return VDS_EC_OK;
+}
+
+int vds_ec_gf8_tables(uint8_t *value2log, uint8_t *log2value) {
+  if (!value2log || !log2value) return VDS_EC_EINVAL;
+  std::memset(value2log, 0, 256);
+  std::memset(log2value, 0, 256);
+  uint32_t v = 1;
+  for (uint32_t l = 0; l < 255; ++l) {
+    log2value[l] = (uint8_t)v;
+    value2log[v] = (uint8_t)l;
+    v = gf8_mul(v, 2);
+  }
+  return VDS_EC_OK;
+}
+
+int vds_ec_multipliers16(uint16_t k, uint16_t node, uint16_t *out) {
+  if (!out && k) return VDS_EC_EINVAL;
+  for (uint32_t j = 0; j < k; ++j) out[j] = gf16_vandermonde(node, j);
+  return VDS_EC_OK;
+}
+
+int vds_ec_multipliers8(uint8_t k, uint8_t node, uint8_t *out) {
+  if (!out && k) return VDS_EC_EINVAL;
+  for (uint32_t j = 0; j < k; ++j) out[j] = j == 0 ? 1 : gf8_pow(node, j);
+  return VDS_EC_OK;
+}
+
+int vds_ec_inverse16(uint16_t k, const uint16_t *nodes, uint16_t *out) {
+  if (k == 0 || !nodes || !out) return VDS_EC_EINVAL;
+  return inverse16(k, nodes, out);
+}
+
+int vds_ec_inverse8(uint8_t k, const uint8_t *nodes, uint8_t *out) {
+  if (k == 0 || !nodes || !out) return VDS_EC_EINVAL;
+  std::vector<uint16_t> m((size_t)k * k);
+  int rc = inverse8(k, nodes, m.data());
+  if (rc) return rc;
+  for (size_t i = 0; i < m.size(); ++i) out[i] = (uint8_t)m[i];
+  return VDS_EC_OK;
+}
+
+int vds_ec_encode16_device(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *in,
+                           uint64_t size, uint64_t in_stride, uint32_t count, uint8_t *const *outs,
+                           uint64_t out_stride, unsigned flags, void *stream) {
+  return encode_device(2, k, replicas, n, in, size, in_stride, count, outs, out_stride, flags, as_stream(stream));
+}
+
+int vds_ec_encode8_device(uint8_t k, const uint8_t *replicas, uint32_t n, const uint8_t *in,
+                          uint64_t size, uint64_t in_stride, uint32_t count, uint8_t *const *outs,
+                          uint64_t out_stride, unsigned flags, void *stream) {
+  if (n > 0 && !replicas) return VDS_EC_EINVAL;
+  std::vector<uint16_t> ids(replicas, replicas + n);
+  return encode_device(1, k, ids.data(), n, in, size, in_stride, count, outs, out_stride, flags, as_stream(stream));
+}
+
+int vds_ec_restore16_device(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks,
+                            uint64_t chunk_size, uint64_t chunk_stride, uint16_t padding,
+                            uint32_t count, uint8_t *out, uint64_t out_stride, unsigned flags,
+                            void *stream) {
+  int rc = check_restore_args(k, nodes, chunks, chunk_size);
+  if (rc) return rc;
+  bool ok = true;
+  const uint64_t len = restored_len(2, k, chunk_size, padding, flags, &ok);
+  if (!ok) return VDS_EC_ERESTORE;
+  if (len && count && !out) return VDS_EC_EINVAL;
+  std::vector<uint16_t> m((size_t)k * k);
+  rc = inverse16(k, nodes, m.data());
+  if (rc) return rc;
+  return restore_device(2, k, m.data(), chunks, chunk_size, chunk_stride, len, count, out, out_stride, flags,
+                        as_stream(stream));
+}
+
+int vds_ec_restore8_device(uint8_t k, const uint8_t *nodes, const uint8_t *const *chunks,
+                           uint64_t chunk_size, uint64_t chunk_stride, uint16_t padding,
+                           uint32_t count, uint8_t *out, uint64_t out_stride, unsigned flags,
+                           void *stream) {
+  int rc = check_restore_args(k, nodes, chunks, chunk_size);
+  if (rc) return rc;
+  bool ok = true;
+  const uint64_t len = restored_len(1, k, chunk_size, padding, flags, &ok);
+  if (!ok) return VDS_EC_ERESTORE;
+  if (len && count && !out) return VDS_EC_EINVAL;
+  std::vector<uint16_t> m((size_t)k * k);
+  rc = inverse8(k, nodes, m.data());
+  if (rc) return rc;
+  return restore_device(1, k, m.data(), chunks, chunk_size, chunk_stride, len, count, out, out_stride, flags,
+                        as_stream(stream));
+}
+
+int vds_ec_encode16_host(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data,
+                         uint64_t size, uint8_t *const *outs, unsigned flags) {
+  return encode_host(2, k, replicas, n, data, size, outs, flags);
+}
+
+int vds_ec_encode8_host(uint8_t k, const uint8_t *replicas, uint32_t n, const uint8_t *data,
+                        uint64_t size, uint8_t *const *outs, unsigned flags) {
+  if (n > 0 && !replicas) return VDS_EC_EINVAL;
+  std::vector<uint16_t> ids(replicas, replicas + n);
+  return encode_host(1, k, ids.data(), n, data, size, outs, flags);
+}
+
+int vds_ec_restore16_host(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks,
+                          uint64_t chunk_size, uint8_t *out, uint64_t *out_size, unsigned flags) {
+  int rc = check_restore_args(k, nodes, chunks, chunk_size);
+  if (rc) return rc;
+  rc = device_ready();
+  if (rc) return rc;
+  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
+  const uint16_t padding =
+      (cells || chunk_size < 2) ? 0 : (uint16_t)((chunks[0][chunk_size - 2] << 8) | chunks[0][chunk_size - 1]);
+  bool ok = true;
+  const uint64_t len = restored_len(2, k, chunk_size, padding, flags, &ok);
+  if (!ok) return VDS_EC_ERESTORE;
+  if (len && !out) return VDS_EC_EINVAL;
+  std::vector<uint16_t> m((size_t)k * k);
+  rc = inverse16(k, nodes, m.data());
+  if (rc) return rc;
+  rc = restore_host(2, k, m.data(), chunks, chunk_size, len, out, flags);
+  if (rc == VDS_EC_OK && out_size) *out_size = len;
+  return rc;
+}
+
+int vds_ec_restore8_host(uint8_t k, const uint8_t *nodes, const uint8_t *const *chunks,
+                         uint64_t chunk_size, uint8_t *out, uint64_t *out_size, unsigned flags) {
+  int rc = check_restore_args(k, nodes, chunks, chunk_size);
+  if (rc) return rc;
+  rc = device_ready();
+  if (rc) return rc;
+  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
+  const uint16_t padding =
+      (cells || chunk_size < 2) ? 0 : (uint16_t)((chunks[0][chunk_size - 2] << 8) | chunks[0][chunk_size - 1]);
+  bool ok = true;
+  const uint64_t len = restored_len(1, k, chunk_size, padding, flags, &ok);
+  if (!ok) return VDS_EC_ERESTORE;
+  if (len && !out) return VDS_EC_EINVAL;
+  std::vector<uint16_t> m((size_t)k * k);
+  rc = inverse8(k, nodes, m.data());
+  if (rc) return rc;
+  rc = restore_host(1, k, m.data(), chunks, chunk_size, len, out, flags);
+  if (rc == VDS_EC_OK && out_size) *out_size = len;
+  return rc;
+}
+
+int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
+                               const uint8_t *const *objs, const uint64_t *sizes, uint32_t count,
+                               uint8_t *const *outs, unsigned flags, int max_devices) {
+  if (k == 0 || (count && (!objs || !sizes || !outs)) || (n && !replicas)) return VDS_EC_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VDS_EC_ENODEV;
+  if (max_devices > 0 && max_devices < ndev) ndev = max_devices;
+  if (count == 0 || n == 0) return VDS_EC_OK;
+  std::atomic<int> status{VDS_EC_OK};
+  auto worker = [&](int dev) {
+    if (hipSetDevice(dev) != hipSuccess) {
+      status = VDS_EC_ENODEV;
+      return;
+    }
+    // Two slots per device: while one slot's object is on the GPU, the
+    // other's pinned staging is being filled / drained by this thread.
+    struct Slot {
+      hipStream_t stream = nullptr;
+      uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+      size_t in_cap = 0, out_cap = 0;
+      int64_t obj = -1;
+    } slot[2];
+    auto release = [&]() {
+      for (auto &s : slot) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.h_in) (void)hipHostFree(s.h_in);
+        if (s.h_out) (void)hipHostFree(s.h_out);
+        if (s.d_in) (void)hipFree(s.d_in);
+        if (s.d_out) (void)hipFree(s.d_out);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+      }
+    };
+    auto drain = [&](Slot &s) -> int {
+      if (s.obj < 0) return VDS_EC_OK;
+      hipError_t e = hipStreamSynchronize(s.stream);
+      if (e != hipSuccess) return hip_status(e);
+      const uint64_t L = vds_ec_replica_size(2, k, sizes[s.obj], flags);
+      for (uint32_t i = 0; i < n; ++i) std::memcpy(outs[(uint64_t)s.obj * n + i], s.h_out + i * L, L);
+      s.obj = -1;
+      return VDS_EC_OK;
+    };
+    int si = 0;
+    for (int64_t o = dev; o < (int64_t)count && status.load() == VDS_EC_OK; o += ndev, si ^= 1) {
+      Slot &s = slot[si];
+      int rc = drain(s);
+      if (rc) { status = rc; break; }
+      const uint64_t size = sizes[o];
+      const uint64_t L = vds_ec_replica_size(2, k, size, flags);
+      const size_t in_b = size ? size : 1, out_b = L * n ? L * n : 1;
+      if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) {
+        status = VDS_EC_ENODEV;
+        break;
+      }
+      if (in_b > s.in_cap) {
+        if (s.h_in) (void)hipHostFree(s.h_in);
+        if (s.d_in) (void)hipFree(s.d_in);
+        s.h_in = s.d_in = nullptr;
+        if (hipHostMalloc(&s.h_in, in_b, 0) != hipSuccess || hipMalloc(&s.d_in, in_b) != hipSuccess) {
+          status = VDS_EC_ENOMEM;
+          break;
+        }
+        s.in_cap = in_b;
+      }
+      if (out_b > s.out_cap) {
+        if (s.h_out) (void)hipHostFree(s.h_out);
+        if (s.d_out) (void)hipFree(s.d_out);
+        s.h_out = s.d_out = nullptr;
+        if (hipHostMalloc(&s.h_out, out_b, 0) != hipSuccess || hipMalloc(&s.d_out, out_b) != hipSuccess) {
+          status = VDS_EC_ENOMEM;
+          break;
+        }
+        s.out_cap = out_b;
+      }
+      if (size) std::memcpy(s.h_in, objs[o], size);
+      hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, size, hipMemcpyHostToDevice, s.stream);
+      if (e != hipSuccess) { status = hip_status(e); break; }
+      std::vector<uint8_t *> douts(n);
+      for (uint32_t i = 0; i < n; ++i) douts[i] = s.d_out + (uint64_t)i * L;
+      rc = encode_device(2, k, replicas, n, s.d_in, size, size, 1, douts.data(), 0, flags, s.stream);
+      if (rc) { status = rc; break; }
+      e = hipMemcpyAsync(s.h_out, s.d_out, L * n, hipMemcpyDeviceToHost, s.stream);
+      if (e != hipSuccess) { status = hip_status(e); break; }
+      s.obj = o;
+    }
+    for (auto &s : slot) {
+      int rc = drain(s);
+      if (rc && status.load() == VDS_EC_OK) status = rc;
+    }
+    release();
+  };
+  std::vector<std::thread> threads;
+  for (int d = 0; d < ndev; ++d) threads.emplace_back(worker, d);
+  for (auto &t : threads) t.join();
+  return status.load();
+}
+
+int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void *stream) {
+  if (size && !dst) return VDS_EC_EINVAL;
+  int rc = device_ready();
+  if (rc) return rc;
+  return hip_status(launch_fill_splitmix(dst, size, seed, as_stream(stream)));
+}
+
+int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint64_t size) {
+  bool contiguous = replicas != nullptr;
+  for (uint32_t i = 0; contiguous && i < n; ++i) contiguous &= (replicas[i] == i);
+  const uint64_t tiles = k ? size / (2ull * k) / kTileStripes : 0;
+  return (contiguous && has_encode_fast(k, n) && tiles > 0) ? 2 : 1;
+}
+
+int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size) {
+  (void)nodes;
+  const uint64_t tiles = (k && chunk_size >= 2) ? ((chunk_size - 2) / 2) / kTileStripes : 0;
+  return (has_restore_fast(k) && tiles > 0) ? 2 : 1;
+}
+
+}  // extern "C"

@@ -116,8 +116,9 @@ int vds_ec_encode16_host(uint16_t k, const uint16_t *replicas, uint32_t n, const
                          uint64_t size, uint8_t *const *outs, unsigned flags);
 int vds_ec_encode8_host(uint8_t k, const uint8_t *replicas, uint32_t n, const uint8_t *data,
                         uint64_t size, uint8_t *const *outs, unsigned flags);
-/* chunks: k host buffers of chunk_size bytes; out must hold
- * (chunk_size-2)*k bytes (chunk_size*k for VDS_EC_F_CELLS); *out_size
+/* chunks: k host buffers of chunk_size bytes; out must hold chunk_size*k
+ * bytes (the most the reference's loop can produce: (chunk_size-2)*k for a
+ * well-formed trailer, more when the trailer is corrupt); *out_size
  * receives the restored length (chunk.h:402-444, chunk_storage.cpp:62-86). */
 int vds_ec_restore16_host(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks,
                           uint64_t chunk_size, uint8_t *out, uint64_t *out_size, unsigned flags);

@@ -72,7 +72,8 @@ int vds_oracle_inverse8(uint8_t k, const uint8_t *nodes, uint8_t *out);
 
 /* chunk.h:402-444 -- decode bytes from k replicas (byte API).
  * chunks[j] pairs with nodes[j]; every chunk has chunk_size bytes.
- * out must hold (chunk_size-2)*k bytes.  Returns the restored size, or
+ * out must hold chunk_size*k bytes (all the reference's loop can produce
+ * before giving up).  Returns the restored size, or
  * (size_t)-1 for the reference's "Fatal error at chunk_restore::restore". */
 size_t vds_oracle_restore16(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks,
                             size_t chunk_size, uint8_t *out);

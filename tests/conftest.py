@@ -16,7 +16,25 @@ for p in (ROOT, TESTS):
         sys.path.insert(0, p)
 
 
+def _dump_runtime_libs():
+    """At exit, record which ROCm shared objects are mapped (one HIP runtime expected)."""
+    out = os.environ.get("VDS_EC_MAPS_DUMP")
+    if not out:
+        return
+    libs = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) >= 6 and any(x in parts[5] for x in ("amdhip", "comgr", "hiprtc", "hsa-runtime",
+                                                               "drm", "vds_ec", "oracle")):
+                libs.add(parts[5])
+    with open(out, "w") as f:
+        f.write("\n".join(sorted(libs)) + "\n")
+
+
 def pytest_configure(config):
+    import atexit
+    atexit.register(_dump_runtime_libs)
     config.addinivalue_line("markers", "gpu: needs a HIP GPU (MI355X); parity tests through the C ABI")
 
 

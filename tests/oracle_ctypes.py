@@ -142,7 +142,7 @@ def restore(k: int, nodes, chunks, cell_bytes: int = 2):
     chunks = [np.ascontiguousarray(c, dtype=np.uint8) for c in chunks]
     size = chunks[0].size
     ptrs = (C.c_void_p * k)(*[_ptr(c) for c in chunks])
-    out = np.empty(max(1, (size - 2) * k if size >= 2 else 1), dtype=np.uint8)
+    out = np.empty(max(1, size * k), dtype=np.uint8)  # the most the reference loop can produce
     fn = lib().vds_oracle_restore16 if cell_bytes == 2 else lib().vds_oracle_restore8
     n = fn(k, nodes.ctypes.data_as(C.POINTER(ct)), ptrs, size, _ptr(out))
     if n == C.c_size_t(-1).value:

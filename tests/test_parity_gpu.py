@@ -236,6 +236,14 @@ def test_restore_error_paths(ec):
     ref = O.restore(4, [1, 2, 3, 4], odd)
     assert ref is not None
     assert np.array_equal(ec.ChunkRestore(4, [1, 2, 3, 4]).restore(odd), ref)
+    # trailer in (2k, 4k]: the reference returns MORE than (size-2)*k bytes,
+    # decoding the trailer row as data
+    long = [c.copy() for c in chunks]
+    for c in long:
+        c[-2:] = [0, 11]
+    ref = O.restore(4, [1, 2, 3, 4], long)
+    assert ref is not None and ref.size == (chunks[0].size - 2) * 4 + 3
+    assert np.array_equal(ec.ChunkRestore(4, [1, 2, 3, 4]).restore(long), ref)
 
 
 # ----------------------------------------------------------- uint8_t / cells

@@ -73,11 +73,27 @@ class VdsEcError(RuntimeError):
         super().__init__(f"{what}: {msg}" if what else msg)
 
 
+def _bind_runtime_first() -> None:
+    """Load torch's HIP runtime before ours when torch is installed.
+
+    torch ships its own libamdhip64.so (soname libamdhip64.so.7) and links it
+    under the unversioned name; if libvds_ec.so (NEEDED libamdhip64.so.7 from
+    /opt/rocm) were loaded first, importing torch afterwards would map a second
+    HIP runtime into the process.  Loading torch first makes our NEEDED entry
+    resolve to the runtime already present, so there is exactly one.
+    """
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
         with _lock:
             if _lib is None:
+                _bind_runtime_first()
                 if not os.path.exists(LIB_PATH):
                     raise RuntimeError(f"{LIB_PATH} is missing: run vds_amd/build.py (no CPU fallback)")
                 h = C.CDLL(LIB_PATH)

@@ -155,7 +155,8 @@ class ChunkRestore:
         size = bufs[0].size
         if any(b.size != size for b in bufs):
             raise VdsEcError(_lib.EINVAL, "chunk_restore::restore")
-        out = np.empty(max(1, (size - 2) * self._k if size >= 2 else 1), dtype=np.uint8)
+        # a corrupt trailer can make the reference return up to size*k bytes (chunk.h:415-441)
+        out = np.empty(max(1, size * self._k), dtype=np.uint8)
         out_size = C.c_uint64(0)
         ptrs = (C.c_void_p * self._k)(*[b.ctypes.data for b in bufs])
         f = _lib.lib().vds_ec_restore16_host if self.cell_bytes == 2 else _lib.lib().vds_ec_restore8_host

@@ -33,11 +33,32 @@ VDS_INLINE Plane16 plane_xor(const Plane16 &a, const Plane16 &b) {
   return r;
 }
 
+VDS_INLINE uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32 (gfx950)
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 VDS_INLINE Plane16 plane_xor3(const Plane16 &a, const Plane16 &b, const Plane16 &c) {
   Plane16 r;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) r.p[i] = a.p[i] ^ b.p[i] ^ c.p[i];
+  for (int i = 0; i < 16; ++i) r.p[i] = xor3(a.p[i], b.p[i], c.p[i]);
   return r;
+}
+
+// acc ^= a & m  (m all-ones or zero; one v_bitop3_b32 per plane on gfx950)
+VDS_INLINE void plane_xor_masked(Plane16 &acc, const Plane16 &a, uint32_t m) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // truth table over S0=0xF0, S1=0xCC, S2=0xAA: S0 ^ (S1 & S2) = 0x78
+    acc.p[i] = __builtin_amdgcn_bitop3_b32(acc.p[i], a.p[i], m, 0x78);
+#else
+    acc.p[i] ^= a.p[i] & m;
+#endif
+  }
 }
 
 VDS_INLINE Plane16 plane_zero() {
@@ -112,16 +133,27 @@ VDS_INLINE Plane16 plane_horner(const Plane16 &acc, const Plane16 &x) {
 }
 
 // Multiply by a wave-uniform runtime constant c (< 2^16): Horner over all 16
-// bit positions.  The x-shift is unconditional so its index rotation stays a
-// static register renaming; only the add is a (uniform) branch on c.
+// bit positions, branch-free (the add is masked by the bit of c).
 VDS_INLINE Plane16 plane_mul_rt(const Plane16 &a, uint32_t c) {
   Plane16 u = plane_zero();
 #pragma unroll
   for (int b = 15; b >= 0; --b) {
     u = plane_mulx(u);
-    if ((c >> b) & 1u) u = plane_xor(u, a);
+    plane_xor_masked(u, a, 0u - ((c >> b) & 1u));
   }
   return u;
+}
+
+// acc[s] ^= c[s] * y for NS runtime constants, sharing the y * x^b chain:
+// y*c = sum_b c_b (y x^b).  Cost: 45 XOR + 16*16*NS masked XOR.
+template <int NS>
+VDS_INLINE void plane_mac_rt(Plane16 (&acc)[NS], Plane16 y, const uint32_t (&c)[NS]) {
+#pragma unroll
+  for (int b = 0; b < 16; ++b) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) plane_xor_masked(acc[s], y, 0u - ((c[s] >> b) & 1u));
+    if (b < 15) y = plane_mulx(y);
+  }
 }
 
 // ---------------------------------------------------------------- transposes

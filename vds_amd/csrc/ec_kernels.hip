@@ -202,7 +202,8 @@ __device__ __forceinline__ void store_replica(const Plane16 &acc, uint8_t *base,
   transpose16x2(rows);
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    const uint32_t nb = (uint32_t)__shfl_xor((int)rows[q], 1);
+    // lane l^1 via DPP quad_perm [1,0,3,2] (no LDS permute)
+    const uint32_t nb = (uint32_t)__builtin_amdgcn_mov_dpp((int)rows[q], 0xB1, 0xF, 0xF, false);
     *reinterpret_cast<uint32_t *>(base + 128 * q) = __builtin_amdgcn_perm(nb, rows[q], sel);
   }
 }
@@ -246,6 +247,28 @@ __device__ __forceinline__ void encode_dispatch(int wave, const uint32_t *set_pl
   }
 }
 
+// Load this wave's word groups of the lane's 32 stripes of `tile`:
+// slot i of lane l <-> stripe stripe0 + l + 64 i.
+template <int K, int G>
+__device__ __forceinline__ void encode_load(uint32_t (&R)[G][32], const FastEncodeArgs &a, uint32_t tile, int lane,
+                                            int wave) {
+  const uint32_t o = tile / a.tiles_per_obj;
+  const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
+  const uint8_t *src = a.in + (uint64_t)o * a.in_stride + (stripe0 + lane) * (2 * K) + 4 * (wave * G);
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const uint8_t *p = src + (uint64_t)i * 64 * (2 * K);
+    if constexpr (G == 2) {
+      const uint2 v = *reinterpret_cast<const uint2 *>(p);
+      R[0][i] = v.x;
+      R[1][i] = v.y;
+    } else {
+#pragma unroll
+      for (int g = 0; g < G; ++g) R[g][i] = *reinterpret_cast<const uint32_t *>(p + 4 * g);
+    }
+  }
+}
+
 template <int K, int N, int RPW>
 __global__ __launch_bounds__((EncodeShape<K, N, RPW>::kThreads), 2) void k_encode_bs(FastEncodeArgs a) {
   using S = EncodeShape<K, N, RPW>;
@@ -255,26 +278,10 @@ __global__ __launch_bounds__((EncodeShape<K, N, RPW>::kThreads), 2) void k_encod
   uint32_t *my_set = lds + lane * S::kSetWords;
   const uint32_t sel = (lane & 1) ? 0x03020706u : 0x05040100u;
 
-  for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
-    const uint32_t o = tile / a.tiles_per_obj;
-    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
-    // ---- load this wave's word groups of the lane's 32 stripes
-    // slot i of lane l <-> stripe stripe0 + l + 64 i
-    const uint8_t *src = a.in + (uint64_t)o * a.in_stride + (stripe0 + lane) * (2 * K) +
-                         4 * (wave * S::kGroupsPerWave);
-    uint32_t R[S::kGroupsPerWave][32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const uint8_t *p = src + (uint64_t)i * 64 * (2 * K);
-      if constexpr (S::kGroupsPerWave == 2) {
-        const uint2 v = *reinterpret_cast<const uint2 *>(p);
-        R[0][i] = v.x;
-        R[1][i] = v.y;
-      } else {
-#pragma unroll
-        for (int g = 0; g < S::kGroupsPerWave; ++g) R[g][i] = *reinterpret_cast<const uint32_t *>(p + 4 * g);
-      }
-    }
+  uint32_t R[S::kGroupsPerWave][32];
+  uint32_t tile = blockIdx.x;
+  if (tile < a.total_tiles) encode_load<K>(R, a, tile, lane, wave);
+  for (; tile < a.total_tiles; tile += gridDim.x) {
     // ---- transpose to planes and publish in LDS: cell 2gw+h, bit b = R[g][16h + (b^8)]
 #pragma unroll
     for (int g = 0; g < S::kGroupsPerWave; ++g) {
@@ -290,7 +297,12 @@ __global__ __launch_bounds__((EncodeShape<K, N, RPW>::kThreads), 2) void k_encod
         }
     }
     __syncthreads();
+    // ---- prefetch the next tile while this one is evaluated (software pipeline)
+    const uint32_t next = tile + gridDim.x;
+    if (next < a.total_tiles) encode_load<K>(R, a, next, lane, wave);
     // ---- evaluate this wave's replicas and store
+    const uint32_t o = tile / a.tiles_per_obj;
+    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
     const uint64_t out_off = (uint64_t)o * a.out_stride +
                              2 * (stripe0 + ((lane & 1) ? (uint64_t)(lane - 1) + 1024 : (uint64_t)lane));
     encode_dispatch<K, N, RPW, 0>(wave, my_set, a, out_off, sel);
@@ -317,6 +329,26 @@ __device__ __forceinline__ uint64_t restore_slot_stripe(int lane, int slot) {
 }
 
 template <int K>
+__device__ __forceinline__ void restore_load(uint32_t (&W)[RestoreShape<K>::kPerWave][16], const FastRestoreArgs &a,
+                                             uint32_t tile, int lane, int wave) {
+  using S = RestoreShape<K>;
+  const uint32_t o = tile / a.tiles_per_obj;
+  const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
+#pragma unroll
+  for (int s = 0; s < S::kPerWave; ++s) {
+    const uint8_t *src = a.chunks[wave * S::kPerWave + s] + (uint64_t)o * a.chunk_stride + 2 * stripe0 + 16 * lane;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(src + 1024 * q);
+      W[s][4 * q + 0] = v.x;
+      W[s][4 * q + 1] = v.y;
+      W[s][4 * q + 2] = v.z;
+      W[s][4 * q + 3] = v.w;
+    }
+  }
+}
+
+template <int K>
 __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(FastRestoreArgs a) {
   using S = RestoreShape<K>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -324,44 +356,37 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t *my_set = lds + lane * S::kSetWords;
 
-  for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
-    const uint32_t o = tile / a.tiles_per_obj;
-    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
-    // ---- load + transpose this wave's survivors
+  uint32_t W[S::kPerWave][16];
+  uint32_t tile = blockIdx.x;
+  if (tile < a.total_tiles) restore_load<K>(W, a, tile, lane, wave);
+  for (; tile < a.total_tiles; tile += gridDim.x) {
+    // ---- transpose this wave's survivors to planes: W[x] = plane of cell bit x^8
 #pragma unroll
     for (int s = 0; s < S::kPerWave; ++s) {
       const int j = wave * S::kPerWave + s;
-      const uint8_t *src = a.chunks[j] + (uint64_t)o * a.chunk_stride + 2 * stripe0 + 16 * lane;
-      uint32_t W[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(src + 1024 * q);
-        W[4 * q + 0] = v.x;
-        W[4 * q + 1] = v.y;
-        W[4 * q + 2] = v.z;
-        W[4 * q + 3] = v.w;
-      }
-      transpose16x2(W);  // W[x] = plane of cell bit x^8
+      transpose16x2(W[s]);
 #pragma unroll
       for (int m = 0; m < 4; ++m)
         *reinterpret_cast<uint4 *>(my_set + j * 16 + 4 * m) =
-            make_uint4(W[4 * (m ^ 2)], W[4 * (m ^ 2) + 1], W[4 * (m ^ 2) + 2], W[4 * (m ^ 2) + 3]);
+            make_uint4(W[s][4 * (m ^ 2)], W[s][4 * (m ^ 2) + 1], W[s][4 * (m ^ 2) + 2], W[s][4 * (m ^ 2) + 3]);
     }
     __syncthreads();
+    const uint32_t next = tile + gridDim.x;
+    if (next < a.total_tiles) restore_load<K>(W, a, next, lane, wave);
     // ---- outputs m = wave*kPerWave + s : sum_j M[m][j] * Y_j
     Plane16 acc[S::kPerWave];
 #pragma unroll
     for (int s = 0; s < S::kPerWave; ++s) acc[s] = plane_zero();
 #pragma clang loop unroll(disable)
     for (int j = 0; j < K; ++j) {
-      const Plane16 y = lds_planes(my_set + j * 16);
+      uint32_t c[S::kPerWave];
 #pragma unroll
-      for (int s = 0; s < S::kPerWave; ++s) {
-        const uint32_t c = a.matrix[(wave * S::kPerWave + s) * K + j];
-        acc[s] = plane_xor(acc[s], plane_mul_rt(y, c));
-      }
+      for (int s = 0; s < S::kPerWave; ++s) c[s] = a.matrix[(wave * S::kPerWave + s) * K + j];
+      plane_mac_rt<S::kPerWave>(acc, lds_planes(my_set + j * 16), c);
     }
     // ---- back to big-endian cells: word group w' = cells (2w', 2w'+1)
+    const uint32_t o = tile / a.tiles_per_obj;
+    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
     uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
 #pragma unroll
     for (int g = 0; g < S::kPerWave / 2; ++g) {
@@ -369,14 +394,20 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) rows[16 * h + j] = acc[2 * g + h].p[j ^ 8];
+        for (int jb = 0; jb < 16; ++jb) rows[16 * h + jb] = acc[2 * g + h].p[jb ^ 8];
       transpose32(rows);
       const int wg = (wave * S::kPerWave) / 2 + g;
+      // slot 8q+e <-> stripe stripe0 + 8 lane + 512 q + e; plane bit pi <-> slot
+      // (pi < 16 ? 2 pi : 2 (pi-16) + 1)
 #pragma unroll
-      for (int pi = 0; pi < 32; ++pi) {
-        const int slot = pi < 16 ? 2 * pi : 2 * (pi - 16) + 1;
-        const uint64_t t = stripe0 + restore_slot_stripe(lane, slot);
-        *reinterpret_cast<uint32_t *>(dst + t * (2 * K) + 4 * wg) = rows[pi];
+      for (int q = 0; q < 4; ++q) {
+        uint8_t *base = dst + (stripe0 + 8u * lane + 512u * q) * (2 * K) + 4 * wg;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int slot = 8 * q + e;
+          const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+          *reinterpret_cast<uint32_t *>(base + e * (2 * K)) = rows[pi];
+        }
       }
     }
     __syncthreads();

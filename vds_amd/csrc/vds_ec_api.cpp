@@ -241,49 +241,42 @@ uint64_t restored_len(unsigned cb, uint32_t k, uint64_t chunk_size, uint16_t pad
 }
 
 // --------------------------------------------------------- host staging
+// Per (thread, device) staging context.  Contexts are never destroyed: they
+// live until process exit, when the HIP runtime reclaims them (freeing them
+// from a thread_local destructor would race the runtime's own teardown).
 struct HostCtx {
-  int device = -1;
   hipStream_t stream = nullptr;
   uint8_t *d_in = nullptr;
   size_t d_in_cap = 0;
   uint8_t *d_out = nullptr;
   size_t d_out_cap = 0;
-  ~HostCtx() {
-    if (device >= 0) {
-      (void)hipSetDevice(device);
-      if (d_in) (void)hipFree(d_in);
-      if (d_out) (void)hipFree(d_out);
-      if (stream) (void)hipStreamDestroy(stream);
+  int grow(uint8_t **p, size_t *cap, size_t want) {
+    if (want <= *cap) return VDS_EC_OK;
+    if (*p) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipFree(*p);
     }
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, want) != hipSuccess) return VDS_EC_ENOMEM;
+    *cap = want;
+    return VDS_EC_OK;
   }
   int ensure(size_t in_bytes, size_t out_bytes) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return VDS_EC_ENODEV;
-    if (dev != device) {
-      this->~HostCtx();
-      new (this) HostCtx();
-      device = dev;
-      if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VDS_EC_ENODEV;
-    }
-    if (in_bytes > d_in_cap) {
-      if (d_in) (void)hipFree(d_in);
-      d_in = nullptr;
-      d_in_cap = 0;
-      if (hipMalloc(&d_in, in_bytes) != hipSuccess) return VDS_EC_ENOMEM;
-      d_in_cap = in_bytes;
-    }
-    if (out_bytes > d_out_cap) {
-      if (d_out) (void)hipFree(d_out);
-      d_out = nullptr;
-      d_out_cap = 0;
-      if (hipMalloc(&d_out, out_bytes) != hipSuccess) return VDS_EC_ENOMEM;
-      d_out_cap = out_bytes;
-    }
-    return VDS_EC_OK;
+    if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VDS_EC_ENODEV;
+    int rc = grow(&d_in, &d_in_cap, in_bytes);
+    return rc ? rc : grow(&d_out, &d_out_cap, out_bytes);
   }
 };
 
-thread_local HostCtx g_host_ctx;
+HostCtx *host_ctx() {
+  thread_local std::vector<HostCtx *> per_device;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
+  if ((size_t)dev >= per_device.size()) per_device.resize(dev + 1, nullptr);
+  if (!per_device[dev]) per_device[dev] = new HostCtx();
+  return per_device[dev];
+}
 
 int encode_host(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data,
                 uint64_t size, uint8_t *const *outs, unsigned flags) {
@@ -292,7 +285,9 @@ int encode_host(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n, c
   if (rc) return rc;
   if (n == 0) return VDS_EC_OK;
   const uint64_t L = vds_ec_replica_size(cb, k, size, flags);
-  HostCtx &c = g_host_ctx;
+  HostCtx *cp = host_ctx();
+  if (!cp) return VDS_EC_ENODEV;
+  HostCtx &c = *cp;
   rc = c.ensure(size ? size : 1, L * n ? L * n : 1);
   if (rc) return rc;
   hipError_t e = hipSuccess;
@@ -311,7 +306,9 @@ int encode_host(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n, c
 
 int restore_host(unsigned cb, uint32_t k, const uint16_t *matrix, const uint8_t *const *chunks,
                  uint64_t chunk_size, uint64_t out_len, uint8_t *out, unsigned flags) {
-  HostCtx &c = g_host_ctx;
+  HostCtx *cp = host_ctx();
+  if (!cp) return VDS_EC_ENODEV;
+  HostCtx &c = *cp;
   const uint64_t in_bytes = chunk_size * k;
   int rc = c.ensure(in_bytes ? in_bytes : 1, out_len ? out_len : 1);
   if (rc) return rc;

@@ -1,0 +1,34 @@
+// chunk_storage.h -- drop-in for lboss75/vds kernel/vds_data/chunk_storage.h
+// (chunk_storage.h:13-34): same class, same signatures.
+#ifndef __VDS_DATA_CHUNK_STORAGE_H_
+#define __VDS_DATA_CHUNK_STORAGE_H_
+
+#include <unordered_map>
+#include <vector>
+
+#include "binary_serialize.h"
+
+namespace vds {
+class _chunk_storage;
+
+class chunk_storage {
+ public:
+  chunk_storage(uint16_t min_horcrux);
+  ~chunk_storage();
+
+  expected<const_data_buffer> generate_replica(uint16_t replica, const void *data, size_t size);
+
+  expected<const_data_buffer> restore_data(const std::unordered_map<uint16_t, const_data_buffer> &horcruxes);
+
+  // Batched form for the save_temp / save_data loops (dht_network_client.cpp:
+  // 74-104, 588-655): every requested replica from one device pass.
+  expected<std::vector<const_data_buffer>> generate_replicas(const std::vector<uint16_t> &replicas,
+                                                             const void *data, size_t size);
+
+ private:
+  friend class ichunk_storage;
+  _chunk_storage *const impl_;
+};
+}  // namespace vds
+
+#endif  // __VDS_DATA_CHUNK_STORAGE_H_

@@ -30,9 +30,21 @@ struct GenericEncodeArgs {
   uint8_t *outs[kMaxLaunchReplicas];
 };
 
+constexpr int kInlineChunks = 64;   // chunk pointers carried in the kernel arguments
+constexpr int kInlineMatrixK = 32;  // k*k inverse carried in the kernel arguments
+
+// Where chunk j lives (first match): chunk_pitch != 0 -> chunk_base + j*pitch
+// (contiguous staging of the host path); chunk_table != nullptr -> device
+// table; otherwise chunk_ptr[j] (k <= kInlineChunks).  The inverse is inline
+// (two coefficients per dword) unless matrix_dev is set.  No stream-ordered
+// allocations are involved, so a launch never depends on a freed table.
 struct GenericRestoreArgs {
-  const uint8_t *const *chunks;  // device array of k pointers
-  const uint16_t *matrix;        // device k*k inverse (row-major)
+  const uint8_t *chunk_ptr[kInlineChunks];
+  const uint8_t *chunk_base;
+  uint64_t chunk_pitch;
+  const uint8_t *const *chunk_table;
+  const uint16_t *matrix_dev;
+  uint32_t matrix_inline[kInlineMatrixK * kInlineMatrixK / 2];
   uint64_t chunk_stride;
   uint32_t count;
   uint32_t k;
@@ -61,7 +73,9 @@ struct FastRestoreArgs {
   uint64_t out_stride;
   uint32_t tiles_per_obj;
   uint32_t total_tiles;
-  uint16_t matrix[kMaxFastK * kMaxFastK];
+  // k x k inverse, row-major, two coefficients per dword (low half = even
+  // column) so the wave-uniform reads are scalar s_load_dword.
+  uint32_t matrix2[kMaxFastK * kMaxFastK / 2];
 };
 
 hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s);

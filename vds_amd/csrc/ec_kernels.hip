@@ -103,15 +103,19 @@ __global__ void k_restore_generic(GenericRestoreArgs a) {
     const uint64_t pos = (t * a.k + m) * CB;
     if (pos >= a.out_len) continue;
     uint32_t acc = 0;
-    const uint16_t *row = a.matrix + (uint64_t)m * a.k;
+    const uint64_t row = (uint64_t)m * a.k;
     for (uint32_t j = 0; j < a.k; ++j) {
-      const uint8_t *c = a.chunks[j] + (uint64_t)o * a.chunk_stride + t * CB;
+      const uint8_t *base = a.chunk_pitch ? a.chunk_base + (uint64_t)j * a.chunk_pitch
+                                          : (a.chunk_table ? a.chunk_table[j] : a.chunk_ptr[j]);
+      const uint8_t *c = base + (uint64_t)o * a.chunk_stride + t * CB;
+      const uint64_t e = row + j;
+      const uint32_t coef = a.matrix_dev ? a.matrix_dev[e] : (a.matrix_inline[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
       uint32_t cell;
       if constexpr (CB == 2)
         cell = native ? (uint32_t)(c[0] | (c[1] << 8)) : (uint32_t)((c[0] << 8) | c[1]);
       else
         cell = c[0];
-      acc ^= gf_mul_cell<CB>(row[j], cell);
+      acc ^= gf_mul_cell<CB>(coef, cell);
     }
     uint8_t *out = a.out + (uint64_t)o * a.out_stride;
     if constexpr (CB == 2) {
@@ -178,12 +182,18 @@ struct EncodeShape {
   static_assert(K % 2 == 0, "fast path needs even k");
 };
 
+// Four ds_read_b128 per cell.  A volatile 128-bit load through an LDS
+// (address_space(3)) pointer keeps the compiler from splitting the reads into
+// ds_read2_b32 / ds_read_b64, which bank-conflict at this padding.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const volatile u32x4 lds_u32x4;
+
 __device__ __forceinline__ Plane16 lds_planes(const uint32_t *p) {
   Plane16 x;
-  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+  lds_u32x4 *q = (lds_u32x4 *)(p);
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
-    const uint4 v = q[m];
+    const u32x4 v = q[m];
     x.p[4 * m + 0] = v.x;
     x.p[4 * m + 1] = v.y;
     x.p[4 * m + 2] = v.z;
@@ -381,7 +391,10 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
     for (int j = 0; j < K; ++j) {
       uint32_t c[S::kPerWave];
 #pragma unroll
-      for (int s = 0; s < S::kPerWave; ++s) c[s] = a.matrix[(wave * S::kPerWave + s) * K + j];
+      for (int s = 0; s < S::kPerWave; ++s) {
+        const uint32_t idx = (wave * S::kPerWave + s) * K + j;
+        c[s] = (a.matrix2[idx >> 1] >> (16 * (idx & 1))) & 0xFFFFu;
+      }
       plane_mac_rt<S::kPerWave>(acc, lds_planes(my_set + j * 16), c);
     }
     // ---- back to big-endian cells: word group w' = cells (2w', 2w'+1)

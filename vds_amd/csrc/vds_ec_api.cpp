@@ -11,6 +11,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -30,6 +32,8 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 
 int hip_status(hipError_t e) {
   if (e == hipSuccess) return VDS_EC_OK;
+  static const bool debug = std::getenv("VDS_EC_DEBUG") != nullptr;
+  if (debug) std::fprintf(stderr, "vds_ec: HIP error %d (%s)\n", (int)e, hipGetErrorString(e));
   if (e == hipErrorOutOfMemory) return VDS_EC_ENOMEM;
   if (e == hipErrorNoDevice || e == hipErrorInvalidDevice || e == hipErrorInsufficientDriver)
     return VDS_EC_ENODEV;
@@ -80,23 +84,6 @@ int inverse8(uint32_t k, const uint8_t *nodes, uint16_t *out) {
       k, a.data(), out, [](uint32_t x, uint32_t y) { return (uint32_t)gf8_mul(x, y); },
       [](uint32_t x) { return (uint32_t)gf8_inv(x); });
 }
-
-// --------------------------------------------------------- device params
-// Small parameter blocks (pointer arrays, k*k matrices) uploaded with
-// stream-ordered allocations so device calls stay asynchronous.
-struct DeviceBlock {
-  void *ptr = nullptr;
-  hipStream_t stream = nullptr;
-  hipError_t upload(const void *host, size_t bytes, hipStream_t s) {
-    stream = s;
-    hipError_t e = hipMallocAsync(&ptr, bytes, s);
-    if (e != hipSuccess) return e;
-    return hipMemcpyAsync(ptr, host, bytes, hipMemcpyHostToDevice, s);
-  }
-  ~DeviceBlock() {
-    if (ptr) (void)hipFreeAsync(ptr, stream);
-  }
-};
 
 // ---------------------------------------------------------- encode core
 int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n, const uint8_t *in,
@@ -161,9 +148,18 @@ int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n,
 }
 
 // --------------------------------------------------------- restore core
+// Optional layout facts the host path knows: chunks contiguous at a pitch,
+// and a device copy of a large inverse already staged.
+struct ChunkLayout {
+  const uint8_t *base = nullptr;
+  uint64_t pitch = 0;
+  const uint16_t *matrix_dev = nullptr;
+};
+
 int restore_device(unsigned cb, uint32_t k, const uint16_t *matrix, const uint8_t *const *chunks,
                    uint64_t chunk_size, uint64_t chunk_stride, uint64_t out_len, uint32_t count,
-                   uint8_t *out, uint64_t out_stride, unsigned flags, hipStream_t s) {
+                   uint8_t *out, uint64_t out_stride, unsigned flags, hipStream_t s,
+                   const ChunkLayout &layout = ChunkLayout()) {
   if (count == 0 || out_len == 0) return VDS_EC_OK;
   int rc = device_ready();
   if (rc) return rc;
@@ -189,31 +185,58 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *matrix, const uint8_
       fa.out_stride = out_stride;
       fa.tiles_per_obj = (uint32_t)tiles;
       fa.total_tiles = (uint32_t)total;
-      std::memcpy(fa.matrix, matrix, sizeof(uint16_t) * k * k);
+      for (uint32_t i = 0; i < k * k; ++i) fa.matrix2[i >> 1] |= uint32_t(matrix[i]) << (16 * (i & 1));
       hipError_t e = launch_restore_fast(k, fa, s);
       if (e != hipSuccess) return hip_status(e);
       fast_stripes = tiles * kTileStripes;
     }
   }
   if (need > fast_stripes) {
-    DeviceBlock dptrs, dmat;
-    hipError_t e = dptrs.upload(chunks, sizeof(uint8_t *) * k, s);
-    if (e == hipSuccess) e = dmat.upload(matrix, sizeof(uint16_t) * (size_t)k * k, s);
-    if (e != hipSuccess) return hip_status(e);
     GenericRestoreArgs ga{};
-    ga.chunks = static_cast<const uint8_t *const *>(dptrs.ptr);
-    ga.matrix = static_cast<const uint16_t *>(dmat.ptr);
-    ga.chunk_stride = chunk_stride;
-    ga.count = count;
-    ga.k = k;
-    ga.cell_bytes = cb;
-    ga.flags = flags;
-    ga.t_begin = fast_stripes;
-    ga.t_count = need - fast_stripes;
-    ga.out = out;
-    ga.out_stride = out_stride;
-    ga.out_len = out_len;
-    e = launch_restore_generic(ga, s);
+    // Temporaries for parameters that do not fit in the kernel arguments;
+    // freed after a stream sync (only reached for k > 32 or k > 64 chunks).
+    void *tmp_table = nullptr, *tmp_matrix = nullptr;
+    hipError_t e = hipSuccess;
+    if (layout.pitch) {
+      ga.chunk_base = layout.base;
+      ga.chunk_pitch = layout.pitch;
+    } else if (k <= (uint32_t)kInlineChunks) {
+      for (uint32_t j = 0; j < k; ++j) ga.chunk_ptr[j] = chunks[j];
+    } else {
+      e = hipMalloc(&tmp_table, sizeof(uint8_t *) * k);
+      if (e == hipSuccess) e = hipMemcpy(tmp_table, chunks, sizeof(uint8_t *) * k, hipMemcpyHostToDevice);
+      ga.chunk_table = static_cast<const uint8_t *const *>(tmp_table);
+    }
+    if (e == hipSuccess) {
+      if (k <= (uint32_t)kInlineMatrixK) {
+        for (uint32_t i = 0; i < k * k; ++i) ga.matrix_inline[i >> 1] |= uint32_t(matrix[i]) << (16 * (i & 1));
+      } else if (layout.matrix_dev) {
+        ga.matrix_dev = layout.matrix_dev;
+      } else {
+        e = hipMalloc(&tmp_matrix, sizeof(uint16_t) * (size_t)k * k);
+        if (e == hipSuccess) e = hipMemcpy(tmp_matrix, matrix, sizeof(uint16_t) * (size_t)k * k, hipMemcpyHostToDevice);
+        ga.matrix_dev = static_cast<const uint16_t *>(tmp_matrix);
+      }
+    }
+    if (e == hipSuccess) {
+      ga.chunk_stride = chunk_stride;
+      ga.count = count;
+      ga.k = k;
+      ga.cell_bytes = cb;
+      ga.flags = flags;
+      ga.t_begin = fast_stripes;
+      ga.t_count = need - fast_stripes;
+      ga.out = out;
+      ga.out_stride = out_stride;
+      ga.out_len = out_len;
+      e = launch_restore_generic(ga, s);
+    }
+    if (tmp_table || tmp_matrix) {
+      const hipError_t se = hipStreamSynchronize(s);
+      if (e == hipSuccess) e = se;
+      if (tmp_table) (void)hipFree(tmp_table);
+      if (tmp_matrix) (void)hipFree(tmp_matrix);
+    }
     if (e != hipSuccess) return hip_status(e);
   }
   return VDS_EC_OK;
@@ -250,6 +273,8 @@ struct HostCtx {
   size_t d_in_cap = 0;
   uint8_t *d_out = nullptr;
   size_t d_out_cap = 0;
+  uint8_t *d_param = nullptr;  // large k x k inverses (k > kInlineMatrixK)
+  size_t d_param_cap = 0;
   int grow(uint8_t **p, size_t *cap, size_t want) {
     if (want <= *cap) return VDS_EC_OK;
     if (*p) {
@@ -312,14 +337,27 @@ int restore_host(unsigned cb, uint32_t k, const uint16_t *matrix, const uint8_t 
   const uint64_t in_bytes = chunk_size * k;
   int rc = c.ensure(in_bytes ? in_bytes : 1, out_len ? out_len : 1);
   if (rc) return rc;
-  std::vector<const uint8_t *> dchunks(k);
+  // chunks staged contiguously: chunk j at d_in + j*chunk_size
   for (uint32_t j = 0; j < k; ++j) {
     hipError_t e = hipMemcpyAsync(c.d_in + (uint64_t)j * chunk_size, chunks[j], chunk_size,
                                   hipMemcpyHostToDevice, c.stream);
     if (e != hipSuccess) return hip_status(e);
-    dchunks[j] = c.d_in + (uint64_t)j * chunk_size;
   }
-  rc = restore_device(cb, k, matrix, dchunks.data(), chunk_size, 0, out_len, 1, c.d_out, 0, flags, c.stream);
+  ChunkLayout layout;
+  layout.base = c.d_in;
+  layout.pitch = chunk_size ? chunk_size : 1;
+  if (k > (uint32_t)kInlineMatrixK) {
+    rc = c.grow(&c.d_param, &c.d_param_cap, sizeof(uint16_t) * (size_t)k * k);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(c.d_param, matrix, sizeof(uint16_t) * (size_t)k * k, hipMemcpyHostToDevice,
+                                  c.stream);
+    if (e != hipSuccess) return hip_status(e);
+    layout.matrix_dev = reinterpret_cast<const uint16_t *>(c.d_param);
+  }
+  std::vector<const uint8_t *> dchunks(k);
+  for (uint32_t j = 0; j < k; ++j) dchunks[j] = c.d_in + (uint64_t)j * chunk_size;
+  rc = restore_device(cb, k, matrix, dchunks.data(), chunk_size, 0, out_len, 1, c.d_out, 0, flags, c.stream,
+                      layout);
   if (rc) return rc;
   if (out_len) {
     hipError_t e = hipMemcpyAsync(out, c.d_out, out_len, hipMemcpyDeviceToHost, c.stream);

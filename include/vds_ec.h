@@ -139,8 +139,11 @@ int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
  * bench.py and the parity tests (SURVEY.md 8(c) "Input PRNG").               */
 int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void *stream);
 
-/* Which kernel path a device call with these parameters takes: 2 = bit-sliced
- * fast path for the full tiles (+ generic tail), 1 = generic path only.     */
+/* Which kernel path a device call with these parameters takes: 3 = syndrome
+ * restore (erasure-pattern-independent XOR programs, survivors within
+ * 0..k+k/4-1) for the full tiles, 2 = bit-sliced fast path for the full tiles
+ * (+ generic tail), 1 = generic path only.  VDS_EC_RESTORE_PATH=bs in the
+ * environment disables path 3 (for A/B measurements).                       */
 int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint64_t size);
 int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size);
 

@@ -199,6 +199,73 @@ def test_fast_restore_tiles_and_tail(ec, k, n):
             assert int(out[size:].sum().item()) == 0  # trimmed to E bytes
 
 
+def _path(k, nodes, L):
+    from vds_amd import _lib
+    arr = np.asarray(nodes, dtype=np.uint16)
+    return _lib.lib().vds_ec_restore16_path(k, arr.ctypes.data_as(_lib.u16p), L)
+
+
+def test_syndrome_restore_erasure_patterns(ec):
+    """k_restore_syn<16,20>: any 16 of the 20 replicas, in any order."""
+    import itertools
+    import torch
+    from vds_amd import chunk
+    k, n = 16, 20
+    size = 2 * 2048 * 2 * k + 2 * k * 5 + 3  # two full tiles + generic tail
+    t = dev_object(torch, size, 2100)
+    enc = dev_encode(torch, k, n, t, size)
+    L = enc.shape[2]
+    rng = np.random.default_rng(21)
+    combos = list(itertools.combinations(range(n), n - k))
+    picks = [combos[0], combos[-1], (0, 5, 10, 15), (16, 17, 18, 19)]
+    picks += [combos[i] for i in rng.choice(len(combos), 300, replace=False)]
+    out = torch.zeros(size + 64, dtype=torch.uint8, device="cuda")
+    for erased in picks:
+        nodes = [r for r in range(n) if r not in erased]
+        rng.shuffle(nodes)
+        assert _path(k, nodes, L) == 3
+        out.zero_()
+        chunk.restore_device(k, nodes, [enc[r, 0].data_ptr() for r in nodes], L, 0, size % (2 * k), 1, out, 0)
+        torch.cuda.synchronize()
+        assert torch.equal(out[:size], t[:size]), erased
+        assert int(out[size:].sum().item()) == 0
+
+
+def test_syndrome_restore_arbitrary_chunks_vs_oracle(ec):
+    """Chunks that are NOT codewords: the result must still be V_S^{-1} applied
+    to the survivors, exactly as the reference's chunk_restore computes it."""
+    import torch
+    from vds_amd import chunk
+    k, n = 16, 20
+    rng = np.random.default_rng(22)
+    for trial in range(6):
+        tiles = int(rng.integers(1, 4))
+        size = tiles * 2048 * 2 * k + int(rng.integers(0, 2 * k * 7))
+        L = chunk.replica_size(k, size)
+        nodes = [int(x) for x in rng.choice(n, k, replace=False)]
+        host = [rng.integers(0, 256, L, dtype=np.uint8) for _ in nodes]
+        pad = size % (2 * k)
+        for c in host:  # a valid trailer, as every replica of one object carries
+            c[-2], c[-1] = pad >> 8, pad & 0xFF
+        ref = O.restore(k, nodes, host)
+        assert ref is not None
+        dev = torch.from_numpy(np.stack(host)).cuda()
+        out = torch.zeros(len(ref) + 64, dtype=torch.uint8, device="cuda")
+        assert _path(k, nodes, L) == 3
+        chunk.restore_device(k, nodes, [dev[j].data_ptr() for j in range(k)], L, 0, pad, 1, out, 0)
+        torch.cuda.synchronize()
+        assert np.array_equal(out[:len(ref)].cpu().numpy(), ref), (trial, nodes)
+
+
+def test_restore_path_selection(ec):
+    L = 2 * 2048 * 2 + 2
+    assert _path(16, list(range(4, 20)), 2 * 2048 * 16 + 2) == 3
+    assert _path(16, list(range(5, 21)), 2 * 2048 * 16 + 2) == 2   # point 20 is outside 0..19
+    assert _path(16, list(range(4, 20)), 2 * 100 + 2) == 1         # no full tile
+    assert _path(32, list(range(8, 40)), 2 * 2048 * 32 + 2) in (2, 3)
+    assert _path(5, list(range(5)), L) == 1
+
+
 def test_restore_device_batched(ec):
     import torch
     from vds_amd import chunk

@@ -78,7 +78,27 @@ struct FastRestoreArgs {
   uint32_t matrix2[kMaxFastK * kMaxFastK / 2];
 };
 
+// Erasure-pattern-independent restore (k_restore_syn<K,N>): survivors are K
+// distinct points of 0..N-1 (N - K == K / 4).  Syndromes and the fixed
+// interpolation are compile-time XOR programs; only the M x M solve
+// c_E = R * S (R = W_E^{-1}) is runtime.
+struct SynRestoreArgs {
+  const uint8_t *chunks[kMaxFastK];  // chunk j holds point point[j]
+  uint8_t point[kMaxFastK];
+  uint8_t erased[kMaxFastK / 4];     // the M erased points
+  uint64_t chunk_stride;
+  uint8_t *out;
+  uint64_t out_stride;
+  uint32_t tiles_per_obj;
+  uint32_t total_tiles;
+  uint32_t solve2[(kMaxFastK / 4) * (kMaxFastK / 4) / 2];  // R, row-major, 2 per dword
+};
+
 hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s);
+bool has_restore_syn(uint32_t k, uint32_t n);
+// W[j][a] = v_a a^j of the syndrome map for (k, n); nullptr if not compiled.
+const uint16_t *restore_syn_weights(uint32_t k, uint32_t n);
+hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s);
 hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s);
 // Returns hipErrorNotSupported when no bit-sliced instantiation exists for (k, n).
 hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, hipStream_t s);

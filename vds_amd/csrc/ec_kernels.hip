@@ -228,9 +228,11 @@ __device__ __forceinline__ void encode_wave_group(const uint32_t *set_planes, co
 #pragma unroll
     for (int s = 0; s < RPW; ++s) acc[s] = x;
   }
+  Plane16 xn = lds_planes(set_planes + (K - 2) * 16);  // one cell ahead: LDS latency under the XORs
 #pragma clang loop unroll(disable)
   for (int c = K - 2; c >= 0; --c) {
-    const Plane16 x = lds_planes(set_planes + c * 16);
+    const Plane16 x = xn;
+    if (c > 0) xn = lds_planes(set_planes + (c - 1) * 16);
     [&]<size_t... I>(std::index_sequence<I...>) {
       ((S::kPlan.rep[W][I] >= 0
             ? (void)(acc[I] = plane_horner<(uint32_t)(S::kPlan.rep[W][I] < 0 ? 0 : S::kPlan.rep[W][I])>(acc[I], x))
@@ -258,23 +260,34 @@ __device__ __forceinline__ void encode_dispatch(int wave, const uint32_t *set_pl
 }
 
 // Load this wave's word groups of the lane's 32 stripes of `tile`:
-// slot i of lane l <-> stripe stripe0 + l + 64 i.
+// slot i of lane l <-> stripe stripe0 + l + 64 i.  The data stays in the
+// loaded vector registers (one uint32 x G vector per slot) until the next
+// iteration unpacks it, so no copy forces an early s_waitcnt.
+template <int G> struct StageVec;
+template <> struct StageVec<1> { typedef uint32_t type; };
+template <> struct StageVec<2> { typedef uint32_t type __attribute__((ext_vector_type(2))); };
+template <> struct StageVec<4> { typedef uint32_t type __attribute__((ext_vector_type(4))); };
+
 template <int K, int G>
-__device__ __forceinline__ void encode_load(uint32_t (&R)[G][32], const FastEncodeArgs &a, uint32_t tile, int lane,
-                                            int wave) {
+__device__ __forceinline__ void encode_load(typename StageVec<G>::type (&P)[32], const FastEncodeArgs &a,
+                                            uint32_t tile, int lane, int wave) {
   const uint32_t o = tile / a.tiles_per_obj;
   const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
   const uint8_t *src = a.in + (uint64_t)o * a.in_stride + (stripe0 + lane) * (2 * K) + 4 * (wave * G);
 #pragma unroll
+  for (int i = 0; i < 32; ++i)
+    P[i] = *reinterpret_cast<const typename StageVec<G>::type *>(src + (uint64_t)i * 64 * (2 * K));
+}
+
+template <int G>
+__device__ __forceinline__ void stage_unpack(const typename StageVec<G>::type (&P)[32], uint32_t (&R)[G][32]) {
+#pragma unroll
   for (int i = 0; i < 32; ++i) {
-    const uint8_t *p = src + (uint64_t)i * 64 * (2 * K);
-    if constexpr (G == 2) {
-      const uint2 v = *reinterpret_cast<const uint2 *>(p);
-      R[0][i] = v.x;
-      R[1][i] = v.y;
+    if constexpr (G == 1) {
+      R[0][i] = P[i];
     } else {
 #pragma unroll
-      for (int g = 0; g < G; ++g) R[g][i] = *reinterpret_cast<const uint32_t *>(p + 4 * g);
+      for (int g = 0; g < G; ++g) R[g][i] = P[i][g];
     }
   }
 }
@@ -288,11 +301,13 @@ __global__ __launch_bounds__((EncodeShape<K, N, RPW>::kThreads), 2) void k_encod
   uint32_t *my_set = lds + lane * S::kSetWords;
   const uint32_t sel = (lane & 1) ? 0x03020706u : 0x05040100u;
 
-  uint32_t R[S::kGroupsPerWave][32];
+  typename StageVec<S::kGroupsPerWave>::type P[32];
   uint32_t tile = blockIdx.x;
-  if (tile < a.total_tiles) encode_load<K>(R, a, tile, lane, wave);
+  if (tile < a.total_tiles) encode_load<K, S::kGroupsPerWave>(P, a, tile, lane, wave);
   for (; tile < a.total_tiles; tile += gridDim.x) {
     // ---- transpose to planes and publish in LDS: cell 2gw+h, bit b = R[g][16h + (b^8)]
+    uint32_t R[S::kGroupsPerWave][32];
+    stage_unpack<S::kGroupsPerWave>(P, R);
 #pragma unroll
     for (int g = 0; g < S::kGroupsPerWave; ++g) {
       transpose32(R[g]);
@@ -309,7 +324,7 @@ __global__ __launch_bounds__((EncodeShape<K, N, RPW>::kThreads), 2) void k_encod
     __syncthreads();
     // ---- prefetch the next tile while this one is evaluated (software pipeline)
     const uint32_t next = tile + gridDim.x;
-    if (next < a.total_tiles) encode_load<K>(R, a, next, lane, wave);
+    if (next < a.total_tiles) encode_load<K, S::kGroupsPerWave>(P, a, next, lane, wave);
     // ---- evaluate this wave's replicas and store
     const uint32_t o = tile / a.tiles_per_obj;
     const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
@@ -339,7 +354,7 @@ __device__ __forceinline__ uint64_t restore_slot_stripe(int lane, int slot) {
 }
 
 template <int K>
-__device__ __forceinline__ void restore_load(uint32_t (&W)[RestoreShape<K>::kPerWave][16], const FastRestoreArgs &a,
+__device__ __forceinline__ void restore_load(u32x4 (&Q)[RestoreShape<K>::kPerWave][4], const FastRestoreArgs &a,
                                              uint32_t tile, int lane, int wave) {
   using S = RestoreShape<K>;
   const uint32_t o = tile / a.tiles_per_obj;
@@ -348,13 +363,7 @@ __device__ __forceinline__ void restore_load(uint32_t (&W)[RestoreShape<K>::kPer
   for (int s = 0; s < S::kPerWave; ++s) {
     const uint8_t *src = a.chunks[wave * S::kPerWave + s] + (uint64_t)o * a.chunk_stride + 2 * stripe0 + 16 * lane;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(src + 1024 * q);
-      W[s][4 * q + 0] = v.x;
-      W[s][4 * q + 1] = v.y;
-      W[s][4 * q + 2] = v.z;
-      W[s][4 * q + 3] = v.w;
-    }
+    for (int q = 0; q < 4; ++q) Q[s][q] = *reinterpret_cast<const u32x4 *>(src + 1024 * q);
   }
 }
 
@@ -366,10 +375,17 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t *my_set = lds + lane * S::kSetWords;
 
-  uint32_t W[S::kPerWave][16];
+  u32x4 Q[S::kPerWave][4];
   uint32_t tile = blockIdx.x;
-  if (tile < a.total_tiles) restore_load<K>(W, a, tile, lane, wave);
+  if (tile < a.total_tiles) restore_load<K>(Q, a, tile, lane, wave);
   for (; tile < a.total_tiles; tile += gridDim.x) {
+    uint32_t W[S::kPerWave][16];
+#pragma unroll
+    for (int s = 0; s < S::kPerWave; ++s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) W[s][4 * q + d] = Q[s][q][d];
     // ---- transpose this wave's survivors to planes: W[x] = plane of cell bit x^8
 #pragma unroll
     for (int s = 0; s < S::kPerWave; ++s) {
@@ -382,20 +398,23 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
     }
     __syncthreads();
     const uint32_t next = tile + gridDim.x;
-    if (next < a.total_tiles) restore_load<K>(W, a, next, lane, wave);
+    if (next < a.total_tiles) restore_load<K>(Q, a, next, lane, wave);
     // ---- outputs m = wave*kPerWave + s : sum_j M[m][j] * Y_j
     Plane16 acc[S::kPerWave];
 #pragma unroll
     for (int s = 0; s < S::kPerWave; ++s) acc[s] = plane_zero();
+    Plane16 yn = lds_planes(my_set);  // one survivor ahead
 #pragma clang loop unroll(disable)
     for (int j = 0; j < K; ++j) {
+      const Plane16 y = yn;
+      if (j + 1 < K) yn = lds_planes(my_set + (j + 1) * 16);
       uint32_t c[S::kPerWave];
 #pragma unroll
       for (int s = 0; s < S::kPerWave; ++s) {
         const uint32_t idx = (wave * S::kPerWave + s) * K + j;
         c[s] = (a.matrix2[idx >> 1] >> (16 * (idx & 1))) & 0xFFFFu;
       }
-      plane_mac_rt<S::kPerWave>(acc, lds_planes(my_set + j * 16), c);
+      plane_mac_rt<S::kPerWave>(acc, y, c);
     }
     // ---- back to big-endian cells: word group w' = cells (2w', 2w'+1)
     const uint32_t o = tile / a.tiles_per_obj;
@@ -412,6 +431,179 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
       const int wg = (wave * S::kPerWave) / 2 + g;
       // slot 8q+e <-> stripe stripe0 + 8 lane + 512 q + e; plane bit pi <-> slot
       // (pi < 16 ? 2 pi : 2 (pi-16) + 1)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint8_t *base = dst + (stripe0 + 8u * lane + 512u * q) * (2 * K) + 4 * wg;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int slot = 8 * q + e;
+          const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+          *reinterpret_cast<uint32_t *>(base + e * (2 * K)) = rows[pi];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================ erasure-pattern-independent restore
+
+template <int K, int N> struct RestorePrograms;
+#include "generated/restore_16_20.inc"
+
+template <int K, int N>
+struct SynShape {
+  static constexpr int kWaves = K / 4;
+  static constexpr int kThreads = 64 * kWaves;
+  static constexpr int kM = N - K;
+  // group-major LDS: plane p = 16 point + bit lives in group p / 4; the four
+  // planes of a group are one 16-byte word per lane, so every access is a
+  // conflict-free ds_{read,write}_b128 (word (p/4)*256 + lane*4 + p%4)
+  static constexpr int kLdsBytes = N * 16 * 64 * 4;
+  static_assert(kM == kWaves, "one syndrome / one erased point per wave");
+};
+
+typedef __attribute__((address_space(3))) volatile u32x4 lds_v4;
+
+// The 16 planes of point `pt` as four b128 LDS accesses.
+__device__ __forceinline__ void syn_put_point(uint32_t *lds, int lane, int pt, const uint32_t (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    lds_v4 *d = (lds_v4 *)(lds + (4 * pt + g) * 256 + 4 * lane);
+    *d = u32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+  }
+}
+
+__device__ __forceinline__ void syn_get_point(const uint32_t *lds, int lane, int pt, uint32_t (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const u32x4 x = *(const lds_v4 *)(lds + (4 * pt + g) * 256 + 4 * lane);
+    v[4 * g] = x[0];
+    v[4 * g + 1] = x[1];
+    v[4 * g + 2] = x[2];
+    v[4 * g + 3] = x[3];
+  }
+}
+
+template <int K, int N, int W>
+__device__ __forceinline__ void syn_dispatch_syndrome(int wave, const uint32_t *lds, int lane, uint32_t (&out)[16]) {
+  if constexpr (W < SynShape<K, N>::kWaves) {
+    if (wave == W) {
+      auto in4 = [lds, lane](int g) -> u32x4 { return *(const lds_v4 *)(lds + g * 256 + 4 * lane); };
+      if constexpr (W == 0) RestorePrograms<K, N>::syndrome0(in4, out);
+      else if constexpr (W == 1) RestorePrograms<K, N>::syndrome1(in4, out);
+      else if constexpr (W == 2) RestorePrograms<K, N>::syndrome2(in4, out);
+      else if constexpr (W == 3) RestorePrograms<K, N>::syndrome3(in4, out);
+    } else {
+      syn_dispatch_syndrome<K, N, W + 1>(wave, lds, lane, out);
+    }
+  }
+}
+
+template <int K, int N, int W>
+__device__ __forceinline__ void syn_dispatch_interp(int wave, const uint32_t *lds, int lane, uint32_t (&out)[64]) {
+  if constexpr (W < SynShape<K, N>::kWaves) {
+    if (wave == W) {
+      auto in4 = [lds, lane](int g) -> u32x4 { return *(const lds_v4 *)(lds + g * 256 + 4 * lane); };
+      if constexpr (W == 0) RestorePrograms<K, N>::interp0(in4, out);
+      else if constexpr (W == 1) RestorePrograms<K, N>::interp1(in4, out);
+      else if constexpr (W == 2) RestorePrograms<K, N>::interp2(in4, out);
+      else if constexpr (W == 3) RestorePrograms<K, N>::interp3(in4, out);
+    } else {
+      syn_dispatch_interp<K, N, W + 1>(wave, lds, lane, out);
+    }
+  }
+}
+
+// Restore of an object from any K of its N replicas without a per-pattern
+// K x K inverse.  Wave w: loads survivors 4w..4w+3 into their points' planes;
+// computes syndrome S_w over all N points (erased points read as zero); solves
+// its erased point c_{e_w} = sum_j R[w][j] S_j (the only runtime-coefficient
+// arithmetic, M multiplies); then interpolates cells 4w..4w+3 from the fixed
+// points 0..K-1 and stores them big-endian.  See tools/xorgen/gen_restore.cpp.
+template <int K, int N>
+__global__ __launch_bounds__((SynShape<K, N>::kThreads), 2) void k_restore_syn(SynRestoreArgs a) {
+  using S = SynShape<K, N>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int kPer = K / S::kWaves;  // survivors loaded per wave (4)
+
+  u32x4 Q[kPer][4];
+  auto load = [&](uint32_t tile) {
+    const uint32_t o = tile / a.tiles_per_obj;
+    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
+#pragma unroll
+    for (int s = 0; s < kPer; ++s) {
+      const uint8_t *src = a.chunks[wave * kPer + s] + (uint64_t)o * a.chunk_stride + 2 * stripe0 + 16 * lane;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Q[s][q] = *reinterpret_cast<const u32x4 *>(src + 1024 * q);
+    }
+  };
+  uint32_t tile = blockIdx.x;
+  if (tile < a.total_tiles) load(tile);
+  const int my_erased = a.erased[wave];
+  for (; tile < a.total_tiles; tile += gridDim.x) {
+    // ---- 1. survivors -> planes of their points; this wave's erased point -> 0
+#pragma unroll
+    for (int s = 0; s < kPer; ++s) {
+      uint32_t W[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) W[4 * q + d] = Q[s][q][d];
+      transpose16x2(W);  // W[x] = plane of cell bit x^8
+      uint32_t P[16];
+#pragma unroll
+      for (int b = 0; b < 16; ++b) P[b] = W[b ^ 8];
+      syn_put_point(lds, lane, a.point[wave * kPer + s], P);
+    }
+    {
+      uint32_t Z[16];
+#pragma unroll
+      for (int b = 0; b < 16; ++b) Z[b] = 0u;
+      syn_put_point(lds, lane, my_erased, Z);
+    }
+    __syncthreads();
+    // ---- 2. syndrome S_wave over all N points
+    uint32_t syn[16];
+    syn_dispatch_syndrome<K, N, 0>(wave, lds, lane, syn);
+    // prefetch the next tile (issued after the syndrome, whose block temps
+    // would otherwise share the register file with the 64 staging registers)
+    const uint32_t next = tile + gridDim.x;
+    if (next < a.total_tiles) load(next);
+    __syncthreads();  // every wave is done reading the zeroed erased planes
+    syn_put_point(lds, lane, my_erased, syn);  // park S_wave in the erased slot
+    __syncthreads();
+    // ---- 3. c_e = sum_j R[wave][j] S_j (e = this wave's erased point)
+    Plane16 ce[1] = {plane_zero()};
+#pragma unroll
+    for (int j = 0; j < S::kM; ++j) {
+      Plane16 sj;
+      syn_get_point(lds, lane, a.erased[j], sj.p);
+      const uint32_t idx = wave * S::kM + j;
+      const uint32_t c[1] = {(a.solve2[idx >> 1] >> (16 * (idx & 1))) & 0xFFFFu};
+      plane_mac_rt<1>(ce, sj, c);
+    }
+    __syncthreads();  // every wave has read all syndromes
+    syn_put_point(lds, lane, my_erased, ce[0].p);
+    __syncthreads();
+    // ---- 4. fixed interpolation from points 0..K-1: cells 4 wave .. 4 wave + 3
+    uint32_t cells[64];
+    syn_dispatch_interp<K, N, 0>(wave, lds, lane, cells);
+    // ---- 5. back to big-endian cells, 2 word groups per wave
+    const uint32_t o = tile / a.tiles_per_obj;
+    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
+    uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      uint32_t rows[32];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int jb = 0; jb < 16; ++jb) rows[16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
+      transpose32(rows);
+      const int wg = 2 * wave + g;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         uint8_t *base = dst + (stripe0 + 8u * lane + 512u * q) * (2 * K) + 4 * wg;
@@ -528,6 +720,37 @@ bool has_restore_fast(uint32_t k) { return k == 16 || k == 32; }
 hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t s) {
   if (k == 16) return launch_restore_bs_k<16>(a, s);
   if (k == 32) return launch_restore_bs_k<32>(a, s);
+  return hipErrorNotSupported;
+}
+
+
+bool has_restore_syn(uint32_t k, uint32_t n) { return k == 16 && n == 20; }
+
+const uint16_t *restore_syn_weights(uint32_t k, uint32_t n) {
+  if (k == 16 && n == 20) return &RestorePrograms<16, 20>::kSyndromeW[0][0];
+  return nullptr;
+}
+
+template <int K, int N>
+static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) {
+  using S = SynShape<K, N>;
+  static bool configured = false;
+  if (!configured) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_restore_syn<K, N>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, S::kLdsBytes);
+    if (e != hipSuccess) return e;
+    configured = true;
+  }
+  const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
+  int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
+  if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_restore_syn<K, N>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s) {
+  if (k == 16 && n == 20) return launch_restore_syn_kn<16, 20>(a, s);
   return hipErrorNotSupported;
 }
 

@@ -85,6 +85,69 @@ int inverse8(uint32_t k, const uint8_t *nodes, uint16_t *out) {
       [](uint32_t x) { return (uint32_t)gf8_inv(x); });
 }
 
+// ------------------------------------------------- syndrome restore plan
+// The erasure-pattern-independent kernel k_restore_syn<K,N> applies when the
+// survivors are K distinct points of 0..N-1 for a compiled (K, N).  The host
+// part is the M x M solve matrix R = W_E^{-1}, W_E[j][i] = v_{e_i} e_i^j
+// (M = N - K, E = the erased points): with S_j = sum_{a survives} W[j][a] c_a,
+// every codeword has sum_a W[j][a] c_a = 0, so W_E c_E = S.  Any K survivor
+// values lie on exactly one polynomial of degree < K, so the recovered
+// replicas and the interpolated object equal V_S^{-1} applied to the
+// survivors (the reference's chunk.h:290-375 route) for every input.
+bool restore_path_override_bs() {
+  static const bool bs = [] {
+    const char *v = std::getenv("VDS_EC_RESTORE_PATH");
+    return v && std::strcmp(v, "bs") == 0;
+  }();
+  return bs;
+}
+
+bool plan_restore_syn(uint32_t k, const uint16_t *nodes, SynRestoreArgs &sa, uint32_t *n_out) {
+  if (!nodes || restore_path_override_bs()) return false;
+  const uint32_t n = k + k / 4;
+  if (k % 4 || !has_restore_syn(k, n)) return false;
+  const uint16_t *W = restore_syn_weights(k, n);
+  const uint32_t m = n - k;
+  std::vector<bool> seen(n, false);
+  for (uint32_t j = 0; j < k; ++j) {
+    if (nodes[j] >= n || seen[nodes[j]]) return false;
+    seen[nodes[j]] = true;
+    sa.point[j] = (uint8_t)nodes[j];
+  }
+  uint32_t e = 0;
+  for (uint32_t a = 0; a < n; ++a)
+    if (!seen[a]) sa.erased[e++] = (uint8_t)a;
+  // Gauss-Jordan on [W_E | I] (m <= 8)
+  std::vector<uint32_t> A((size_t)m * 2 * m, 0);
+  for (uint32_t j = 0; j < m; ++j) {
+    for (uint32_t i = 0; i < m; ++i) A[j * 2 * m + i] = W[j * n + sa.erased[i]];
+    A[j * 2 * m + m + j] = 1;
+  }
+  for (uint32_t c = 0; c < m; ++c) {
+    uint32_t piv = c;
+    while (piv < m && A[piv * 2 * m + c] == 0) ++piv;
+    if (piv == m) return false;  // cannot happen for distinct points
+    if (piv != c)
+      for (uint32_t x = 0; x < 2 * m; ++x) std::swap(A[c * 2 * m + x], A[piv * 2 * m + x]);
+    const uint32_t iv = gf16_inv(A[c * 2 * m + c]);
+    for (uint32_t x = 0; x < 2 * m; ++x) A[c * 2 * m + x] = gf16_mul(A[c * 2 * m + x], iv);
+    for (uint32_t r = 0; r < m; ++r) {
+      const uint32_t f = A[r * 2 * m + c];
+      if (r == c || f == 0) continue;
+      for (uint32_t x = 0; x < 2 * m; ++x) A[r * 2 * m + x] ^= gf16_mul(f, A[c * 2 * m + x]);
+    }
+  }
+  // R[i][j]: row i = the erased point the kernel's wave i recovers
+  std::memset(sa.solve2, 0, sizeof sa.solve2);
+  for (uint32_t i = 0; i < m; ++i)
+    for (uint32_t j = 0; j < m; ++j) {
+      const uint32_t idx = i * m + j;
+      sa.solve2[idx >> 1] |= A[i * 2 * m + m + j] << (16 * (idx & 1));
+    }
+  *n_out = n;
+  return true;
+}
+
 // ---------------------------------------------------------- encode core
 int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n, const uint8_t *in,
                   uint64_t size, uint64_t in_stride, uint32_t count, uint8_t *const *outs,
@@ -156,7 +219,7 @@ struct ChunkLayout {
   const uint16_t *matrix_dev = nullptr;
 };
 
-int restore_device(unsigned cb, uint32_t k, const uint16_t *matrix, const uint8_t *const *chunks,
+int restore_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_t *matrix, const uint8_t *const *chunks,
                    uint64_t chunk_size, uint64_t chunk_stride, uint64_t out_len, uint32_t count,
                    uint8_t *out, uint64_t out_stride, unsigned flags, hipStream_t s,
                    const ChunkLayout &layout = ChunkLayout()) {
@@ -173,7 +236,24 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *matrix, const uint8_
   if (need > cells_per_chunk) need = cells_per_chunk;
 
   uint64_t fast_stripes = 0;
-  if (cb == 2 && !cells && has_restore_fast(k)) {
+  SynRestoreArgs sa{};
+  uint32_t syn_n = 0;
+  const bool syn = cb == 2 && !cells && plan_restore_syn(k, nodes, sa, &syn_n);
+  if (syn) {
+    const uint64_t tiles = (out_len / stripe_bytes) / kTileStripes;
+    const uint64_t total = tiles * count;
+    if (tiles > 0 && total <= 0xFFFFFFFFull) {
+      for (uint32_t j = 0; j < k; ++j) sa.chunks[j] = chunks[j];
+      sa.chunk_stride = chunk_stride;
+      sa.out = out;
+      sa.out_stride = out_stride;
+      sa.tiles_per_obj = (uint32_t)tiles;
+      sa.total_tiles = (uint32_t)total;
+      hipError_t e = launch_restore_syn(k, syn_n, sa, s);
+      if (e != hipSuccess) return hip_status(e);
+      fast_stripes = tiles * kTileStripes;
+    }
+  } else if (cb == 2 && !cells && has_restore_fast(k)) {
     const uint64_t full = out_len / stripe_bytes;
     const uint64_t tiles = full / kTileStripes;
     const uint64_t total = tiles * count;
@@ -329,7 +409,7 @@ int encode_host(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n, c
   return hip_status(hipStreamSynchronize(c.stream));
 }
 
-int restore_host(unsigned cb, uint32_t k, const uint16_t *matrix, const uint8_t *const *chunks,
+int restore_host(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_t *matrix, const uint8_t *const *chunks,
                  uint64_t chunk_size, uint64_t out_len, uint8_t *out, unsigned flags) {
   HostCtx *cp = host_ctx();
   if (!cp) return VDS_EC_ENODEV;
@@ -356,7 +436,7 @@ int restore_host(unsigned cb, uint32_t k, const uint16_t *matrix, const uint8_t 
   }
   std::vector<const uint8_t *> dchunks(k);
   for (uint32_t j = 0; j < k; ++j) dchunks[j] = c.d_in + (uint64_t)j * chunk_size;
-  rc = restore_device(cb, k, matrix, dchunks.data(), chunk_size, 0, out_len, 1, c.d_out, 0, flags, c.stream,
+  rc = restore_device(cb, k, nodes, matrix, dchunks.data(), chunk_size, 0, out_len, 1, c.d_out, 0, flags, c.stream,
                       layout);
   if (rc) return rc;
   if (out_len) {
@@ -498,7 +578,7 @@ int vds_ec_restore16_device(uint16_t k, const uint16_t *nodes, const uint8_t *co
   std::vector<uint16_t> m((size_t)k * k);
   rc = inverse16(k, nodes, m.data());
   if (rc) return rc;
-  return restore_device(2, k, m.data(), chunks, chunk_size, chunk_stride, len, count, out, out_stride, flags,
+  return restore_device(2, k, nodes, m.data(), chunks, chunk_size, chunk_stride, len, count, out, out_stride, flags,
                         as_stream(stream));
 }
 
@@ -515,7 +595,7 @@ int vds_ec_restore8_device(uint8_t k, const uint8_t *nodes, const uint8_t *const
   std::vector<uint16_t> m((size_t)k * k);
   rc = inverse8(k, nodes, m.data());
   if (rc) return rc;
-  return restore_device(1, k, m.data(), chunks, chunk_size, chunk_stride, len, count, out, out_stride, flags,
+  return restore_device(1, k, nullptr, m.data(), chunks, chunk_size, chunk_stride, len, count, out, out_stride, flags,
                         as_stream(stream));
 }
 
@@ -547,7 +627,7 @@ int vds_ec_restore16_host(uint16_t k, const uint16_t *nodes, const uint8_t *cons
   std::vector<uint16_t> m((size_t)k * k);
   rc = inverse16(k, nodes, m.data());
   if (rc) return rc;
-  rc = restore_host(2, k, m.data(), chunks, chunk_size, len, out, flags);
+  rc = restore_host(2, k, nodes, m.data(), chunks, chunk_size, len, out, flags);
   if (rc == VDS_EC_OK && out_size) *out_size = len;
   return rc;
 }
@@ -568,7 +648,7 @@ int vds_ec_restore8_host(uint8_t k, const uint8_t *nodes, const uint8_t *const *
   std::vector<uint16_t> m((size_t)k * k);
   rc = inverse8(k, nodes, m.data());
   if (rc) return rc;
-  rc = restore_host(1, k, m.data(), chunks, chunk_size, len, out, flags);
+  rc = restore_host(1, k, nullptr, m.data(), chunks, chunk_size, len, out, flags);
   if (rc == VDS_EC_OK && out_size) *out_size = len;
   return rc;
 }
@@ -684,9 +764,12 @@ int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint6
 }
 
 int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size) {
-  (void)nodes;
   const uint64_t tiles = (k && chunk_size >= 2) ? ((chunk_size - 2) / 2) / kTileStripes : 0;
-  return (has_restore_fast(k) && tiles > 0) ? 2 : 1;
+  if (tiles == 0) return 1;
+  SynRestoreArgs sa{};
+  uint32_t n = 0;
+  if (plan_restore_syn(k, nodes, sa, &n)) return 3;
+  return has_restore_fast(k) ? 2 : 1;
 }
 
 }  // extern "C"

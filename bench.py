@@ -41,7 +41,9 @@ def parse():
     p.add_argument("--object-mib", type=float, default=64.0)
     p.add_argument("--erase", type=str, default="", help="comma list of erased replica ids")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-objects", type=int, default=3, help="objects in the CPU baseline sample")
+    p.add_argument("--cpu-objects", type=int, default=8, help="objects in the CPU baseline sample")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="per-object HBM bytes per kernel from rocprofv3 PMC passes (tools/pmc_traffic.py)")
     return p.parse_args()
 
 
@@ -71,6 +73,34 @@ def cpu_baseline(k, n, size, nodes, count):
             "sample": f"{count} x {size >> 20} MiB objects, encode all {n} replicas + repair from {len(nodes)} "
                       f"(oracle/vds_oracle.c, 1 thread, {dt:.2f} s)",
             "seconds": round(dt, 3)}
+
+
+def kernel_names(k, n, nodes, size, L):
+    """Names of the kernels the C ABI dispatches for this workload."""
+    import ctypes as C
+    import numpy as np
+    from vds_amd import _lib
+    ids = np.arange(n, dtype=np.uint16)
+    nd = np.asarray(nodes, dtype=np.uint16)
+    ep = _lib.lib().vds_ec_encode16_path(k, ids.ctypes.data_as(_lib.u16p), n, C.c_uint64(size))
+    rp = _lib.lib().vds_ec_restore16_path(k, nd.ctypes.data_as(_lib.u16p), C.c_uint64(L))
+    enc = {2: f"k_encode_bs<{k},{n}>"}.get(ep, "k_encode_generic")
+    rep = {3: f"k_restore_syn<{k},{n}>", 2: f"k_restore_bs<{k}>"}.get(rp, "k_restore_generic")
+    return enc, rep
+
+
+def pmc_traffic(path, kernel, objects):
+    """roofline.traffic: HBM bytes per launch of `kernel` from the committed
+    rocprofv3 FETCH_SIZE/WRITE_SIZE passes (bytes per object x objects)."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    e = t.get(kernel.split("<")[0])
+    if not e:
+        return None, None
+    return round(e["bytes_per_object"] * objects), f"{os.path.relpath(path, ROOT)}: {e['source']}"
 
 
 def main():
@@ -166,11 +196,13 @@ def main():
 
     enc_bytes = objects * (size + n * L)      # S + n*(2*ceil(S/2k)+2)
     rep_bytes = objects * (k * L + size)      # k*L + S
+    enc_name, rep_name = kernel_names(k, n, nodes, size, L)
     if enc_ms >= rep_ms:
-        dom, dom_bytes, dom_ms = "k_encode_bs<16,20,5>" if (k, n) == (16, 20) else "k_encode_bs", enc_bytes, enc_ms
+        dom, dom_bytes, dom_ms = enc_name, enc_bytes, enc_ms
     else:
-        dom, dom_bytes, dom_ms = "k_restore_bs<16>" if k == 16 else "k_restore_bs", rep_bytes, rep_ms
+        dom, dom_bytes, dom_ms = rep_name, rep_bytes, rep_ms
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.traffic_json, dom, objects)
 
     result = {
         "metric": "device-resident encode+repair GiB/s, k=16 m=4 64 MiB stripes, 1/2/4/8 GPU",
@@ -194,8 +226,9 @@ def main():
         "encode_ms": round(enc_ms, 3),
         "repair_ms": round(rep_ms, 3),
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4)},
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src, "algorithmic_bytes_per_launch": dom_bytes,
+                     "avg_launch_ms": round(dom_ms, 4), "kernels": {"encode": enc_name, "repair": rep_name}},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -91,7 +91,9 @@ struct SynRestoreArgs {
   uint64_t out_stride;
   uint32_t tiles_per_obj;
   uint32_t total_tiles;
-  uint32_t solve2[(kMaxFastK / 4) * (kMaxFastK / 4) / 2];  // R, row-major, 2 per dword
+  // R = W_E^{-1} as bit selections: byte (b & 3) of solve_sel[i][b >> 2] has
+  // bit j set iff bit b of R[i][j] is set (row i = erased[i], M <= 8)
+  uint32_t solve_sel[kMaxFastK / 4][4];
 };
 
 hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s);

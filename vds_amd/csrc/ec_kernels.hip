@@ -485,32 +485,45 @@ __device__ __forceinline__ void syn_get_point(const uint32_t *lds, int lane, int
   }
 }
 
+// Group g of the plane-major LDS as seen by one lane.  ds_read_b128 carries a
+// 16-bit immediate offset, so groups past 64 KiB (points >= 16) are addressed
+// from a second base register; the base is laundered through an empty asm so
+// the compiler does not fold it back into one address register per group.
+typedef __attribute__((address_space(3))) char lds_char;
+struct SynLds {
+  lds_char *base;
+  uint32_t lo;  // 16 * lane
+  uint32_t hi;  // 16 * lane + 64 KiB (opaque)
+  __device__ __forceinline__ u32x4 operator()(int g) const {
+    if (g < 64) return *(lds_v4 *)(base + lo + g * 1024);
+    return *(lds_v4 *)(base + hi + (g - 64) * 1024);
+  }
+};
+
 template <int K, int N, int W>
-__device__ __forceinline__ void syn_dispatch_syndrome(int wave, const uint32_t *lds, int lane, uint32_t (&out)[16]) {
+__device__ __forceinline__ void syn_dispatch_syndrome(int wave, const SynLds &in4, uint32_t (&out)[16]) {
   if constexpr (W < SynShape<K, N>::kWaves) {
     if (wave == W) {
-      auto in4 = [lds, lane](int g) -> u32x4 { return *(const lds_v4 *)(lds + g * 256 + 4 * lane); };
       if constexpr (W == 0) RestorePrograms<K, N>::syndrome0(in4, out);
       else if constexpr (W == 1) RestorePrograms<K, N>::syndrome1(in4, out);
       else if constexpr (W == 2) RestorePrograms<K, N>::syndrome2(in4, out);
       else if constexpr (W == 3) RestorePrograms<K, N>::syndrome3(in4, out);
     } else {
-      syn_dispatch_syndrome<K, N, W + 1>(wave, lds, lane, out);
+      syn_dispatch_syndrome<K, N, W + 1>(wave, in4, out);
     }
   }
 }
 
 template <int K, int N, int W>
-__device__ __forceinline__ void syn_dispatch_interp(int wave, const uint32_t *lds, int lane, uint32_t (&out)[64]) {
+__device__ __forceinline__ void syn_dispatch_interp(int wave, const SynLds &in4, uint32_t (&out)[64]) {
   if constexpr (W < SynShape<K, N>::kWaves) {
     if (wave == W) {
-      auto in4 = [lds, lane](int g) -> u32x4 { return *(const lds_v4 *)(lds + g * 256 + 4 * lane); };
       if constexpr (W == 0) RestorePrograms<K, N>::interp0(in4, out);
       else if constexpr (W == 1) RestorePrograms<K, N>::interp1(in4, out);
       else if constexpr (W == 2) RestorePrograms<K, N>::interp2(in4, out);
       else if constexpr (W == 3) RestorePrograms<K, N>::interp3(in4, out);
     } else {
-      syn_dispatch_interp<K, N, W + 1>(wave, lds, lane, out);
+      syn_dispatch_interp<K, N, W + 1>(wave, in4, out);
     }
   }
 }
@@ -540,6 +553,11 @@ __global__ __launch_bounds__((SynShape<K, N>::kThreads), 2) void k_restore_syn(S
       for (int q = 0; q < 4; ++q) Q[s][q] = *reinterpret_cast<const u32x4 *>(src + 1024 * q);
     }
   };
+  SynLds in4;
+  in4.base = (lds_char *)lds;
+  in4.lo = 16u * lane;
+  in4.hi = 16u * lane + 65536u;
+  asm volatile("" : "+v"(in4.hi));
   uint32_t tile = blockIdx.x;
   if (tile < a.total_tiles) load(tile);
   const int my_erased = a.erased[wave];
@@ -567,7 +585,7 @@ __global__ __launch_bounds__((SynShape<K, N>::kThreads), 2) void k_restore_syn(S
     __syncthreads();
     // ---- 2. syndrome S_wave over all N points
     uint32_t syn[16];
-    syn_dispatch_syndrome<K, N, 0>(wave, lds, lane, syn);
+    syn_dispatch_syndrome<K, N, 0>(wave, in4, syn);
     // prefetch the next tile (issued after the syndrome, whose block temps
     // would otherwise share the register file with the 64 staging registers)
     const uint32_t next = tile + gridDim.x;
@@ -575,44 +593,57 @@ __global__ __launch_bounds__((SynShape<K, N>::kThreads), 2) void k_restore_syn(S
     __syncthreads();  // every wave is done reading the zeroed erased planes
     syn_put_point(lds, lane, my_erased, syn);  // park S_wave in the erased slot
     __syncthreads();
-    // ---- 3. c_e = sum_j R[wave][j] S_j (e = this wave's erased point)
-    Plane16 ce[1] = {plane_zero()};
+    // ---- 3. c_e = sum_j R[wave][j] S_j (e = this wave's erased point), by
+    // Horner over the 16 coefficient bits: ce = ce * x, then add the S_j whose
+    // coefficient has that bit set.  The selections are wave-uniform bytes
+    // (host-precomputed), so the adds are scalar branches over plain XORs.
+    Plane16 sy[S::kM];
 #pragma unroll
-    for (int j = 0; j < S::kM; ++j) {
-      Plane16 sj;
-      syn_get_point(lds, lane, a.erased[j], sj.p);
-      const uint32_t idx = wave * S::kM + j;
-      const uint32_t c[1] = {(a.solve2[idx >> 1] >> (16 * (idx & 1))) & 0xFFFFu};
-      plane_mac_rt<1>(ce, sj, c);
-    }
+    for (int j = 0; j < S::kM; ++j) syn_get_point(lds, lane, a.erased[j], sy[j].p);
     __syncthreads();  // every wave has read all syndromes
-    syn_put_point(lds, lane, my_erased, ce[0].p);
+    Plane16 ce = plane_zero();
+#pragma unroll
+    for (int b = 15; b >= 0; --b) {
+      if (b != 15) ce = plane_mulx(ce);
+      const uint32_t sel = (a.solve_sel[wave][b >> 2] >> (8 * (b & 3))) & 0xFFu;
+#pragma unroll
+      for (int j = 0; j < S::kM; j += 2) {
+        const uint32_t two = (sel >> j) & 3u;
+        if (two == 1u)
+          ce = plane_xor(ce, sy[j]);
+        else if (two == 2u)
+          ce = plane_xor(ce, sy[j + 1]);
+        else if (two == 3u)
+          ce = plane_xor3(ce, sy[j], sy[j + 1]);
+      }
+    }
+    syn_put_point(lds, lane, my_erased, ce.p);
     __syncthreads();
     // ---- 4. fixed interpolation from points 0..K-1: cells 4 wave .. 4 wave + 3
     uint32_t cells[64];
-    syn_dispatch_interp<K, N, 0>(wave, lds, lane, cells);
-    // ---- 5. back to big-endian cells, 2 word groups per wave
+    syn_dispatch_interp<K, N, 0>(wave, in4, cells);
+    // ---- 5. back to big-endian cells: word groups 2 wave, 2 wave + 1 (cells
+    // 4 wave .. 4 wave + 3, 8 contiguous bytes of every stripe) as 8-byte stores
     const uint32_t o = tile / a.tiles_per_obj;
     const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
     uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
+    uint32_t rows[2][32];
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      uint32_t rows[32];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int jb = 0; jb < 16; ++jb) rows[16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
-      transpose32(rows);
-      const int wg = 2 * wave + g;
+        for (int jb = 0; jb < 16; ++jb) rows[g][16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
+      transpose32(rows[g]);
+    }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint8_t *base = dst + (stripe0 + 8u * lane + 512u * q) * (2 * K) + 4 * wg;
+    for (int q = 0; q < 4; ++q) {
+      uint8_t *base = dst + (stripe0 + 8u * lane + 512u * q) * (2 * K) + 8 * wave;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int slot = 8 * q + e;
-          const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
-          *reinterpret_cast<uint32_t *>(base + e * (2 * K)) = rows[pi];
-        }
+      for (int e = 0; e < 8; ++e) {
+        const int slot = 8 * q + e;
+        const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+        *reinterpret_cast<uint2 *>(base + e * (2 * K)) = make_uint2(rows[0][pi], rows[1][pi]);
       }
     }
     __syncthreads();

@@ -138,11 +138,12 @@ bool plan_restore_syn(uint32_t k, const uint16_t *nodes, SynRestoreArgs &sa, uin
     }
   }
   // R[i][j]: row i = the erased point the kernel's wave i recovers
-  std::memset(sa.solve2, 0, sizeof sa.solve2);
+  std::memset(sa.solve_sel, 0, sizeof sa.solve_sel);
   for (uint32_t i = 0; i < m; ++i)
     for (uint32_t j = 0; j < m; ++j) {
-      const uint32_t idx = i * m + j;
-      sa.solve2[idx >> 1] |= A[i * 2 * m + m + j] << (16 * (idx & 1));
+      const uint32_t r = A[i * 2 * m + m + j];
+      for (uint32_t b = 0; b < 16; ++b)
+        if ((r >> b) & 1u) sa.solve_sel[i][b >> 2] |= 1u << (8 * (b & 3) + j);
     }
   *n_out = n;
   return true;

@@ -1,0 +1,46 @@
+"""Time the encode and repair launches on a resident batch (no correctness
+check: used for A/B of diagnostic variant builds via VDS_EC_LIB).
+
+  python tools/time_kernels.py [--objects 128] [--iters 5]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+from vds_amd import chunk  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--objects", type=int, default=128)
+p.add_argument("--iters", type=int, default=5)
+p.add_argument("--tag", default=os.path.basename(os.environ.get("VDS_EC_LIB", "default")))
+a = p.parse_args()
+k, n, size = 16, 20, 64 << 20
+L = chunk.replica_size(k, size)
+inp = torch.empty(a.objects * size, dtype=torch.uint8, device="cuda")
+reps = torch.empty((n, a.objects * L), dtype=torch.uint8, device="cuda")
+out = torch.empty(a.objects * size, dtype=torch.uint8, device="cuda")
+for i in range(a.objects):
+    chunk.fill_splitmix_device(inp[i * size:], size, 0x7664730000000000 + i)
+nodes = [r for r in range(n) if r not in (0, 5, 10, 15)]
+rp = [reps[i].data_ptr() for i in range(n)]
+cp = [reps[r].data_ptr() for r in nodes]
+enc = lambda: chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, rp, L)  # noqa: E731
+rep = lambda: chunk.restore_device(k, nodes, cp, L, L, size % (2 * k), a.objects, out, size)  # noqa: E731
+enc()
+rep()
+torch.cuda.synchronize()
+res = {}
+for name, f in (("encode", enc), ("repair", rep)):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.iters
+    res[name] = (ms, a.objects * size / (ms * 1e-3) / 2**30)
+print(f"{a.tag}: encode {res['encode'][0]:.3f} ms ({res['encode'][1]:.1f} GiB/s)  "
+      f"repair {res['repair'][0]:.3f} ms ({res['repair'][1]:.1f} GiB/s)", flush=True)

@@ -5,7 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
-enum Op { XOR2, BITOP3_V, BITOP3_S, BFI, PERM };
+enum Op { XOR2, BITOP3_V, BITOP3_S, BFI, PERM, PERM_V, LSHL, BITOP3_LIT, ALIGNBIT, DPP, AND_LIT, LSHL_OR };
 
 template <int OP>
 __global__ __launch_bounds__(1024) void k_rate(uint32_t *out, uint32_t seed, int iters) {
@@ -29,6 +29,14 @@ __global__ __launch_bounds__(1024) void k_rate(uint32_t *out, uint32_t seed, int
           asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(v[c]) : "v"(w[c]), "s"(k));
         if constexpr (OP == BFI) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % C]));
         if constexpr (OP == PERM) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "s"(k));
+        if constexpr (OP == PERM_V) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % C]));
+        if constexpr (OP == LSHL) asm volatile("v_lshlrev_b32 %0, 4, %0" : "+v"(v[c]));
+        if constexpr (OP == BITOP3_LIT)
+          asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(v[c]) : "v"(w[c]), "v"(k));
+        if constexpr (OP == ALIGNBIT) asm volatile("v_alignbit_b32 %0, %0, %1, 4" : "+v"(v[c]) : "v"(w[c]));
+        if constexpr (OP == DPP) asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(v[c]) : "v"(w[c]));
+        if constexpr (OP == AND_LIT) asm volatile("v_and_b32 %0, 0x0f0f0f0f, %0" : "+v"(v[c]));
+        if constexpr (OP == LSHL_OR) asm volatile("v_lshl_or_b32 %0, %0, 4, %1" : "+v"(v[c]) : "v"(w[c]));
       }
     // keep w live and changing so nothing is hoisted
 #pragma unroll
@@ -63,12 +71,19 @@ static void run(const char *name, int waves_per_cu) {
 }
 
 int main() {
-  for (int w : {4, 8, 16}) {
+  for (int w : {8, 16}) {
     run<XOR2>("xor2", w);
     run<BITOP3_V>("bitop3_v", w);
     run<BITOP3_S>("bitop3_s", w);
+    run<BITOP3_LIT>("bfi_as_bitop3_vmask", w);
     run<BFI>("bfi", w);
-    run<PERM>("perm", w);
+    run<PERM>("perm_s", w);
+    run<PERM_V>("perm_v", w);
+    run<LSHL>("lshl", w);
+    run<ALIGNBIT>("alignbit", w);
+    run<DPP>("mov_dpp", w);
+    run<AND_LIT>("and_lit", w);
+    run<LSHL_OR>("lshl_or", w);
   }
   return 0;
 }

@@ -44,41 +44,91 @@ static std::vector<std::vector<int>> bitrows(const std::vector<uint32_t> &M, int
   return out;
 }
 
-// Emit one block of a program: the block reads the input planes of points
-// [p0, p0 + np) (IN4(g) = the 4 planes of group g, a b128 LDS read) and
-// accumulates its share into acc[]; `first` assigns instead.  Temps are emitted
-// in creation order and each output row is folded in as soon as everything it
-// needs exists, so temps die early and register pressure stays bounded.
-static size_t emit_block(const xorgen::XorProgram &p, int p0, bool first) {
+// One block of a program: a Paar program over the input planes of points
+// [p0, p0 + np), turned into emit-ready nodes.  Single-use two-input temps are
+// fused into their consumer, so most nodes become one v_bitop3_b32 (a 3-input
+// XOR at the issue cost of a 2-input one on gfx950).
+struct Block {
+  int p0 = 0, n = 0;
+  std::vector<std::vector<int>> node;  // operands per temp id (n + t); empty = fused away
+  std::vector<std::vector<int>> rows;  // operands per output row (expanded)
+  std::vector<bool> group_used;
+};
+
+static Block make_block(const xorgen::XorProgram &p, int p0) {
+  Block B;
+  B.p0 = p0;
+  B.n = p.ninputs;
   const int n = p.ninputs, T = (int)p.temps.size();
-  std::vector<bool> used(n, false);
-  for (auto &t : p.temps) {
-    if (t.first < n) used[t.first] = true;
-    if (t.second < n) used[t.second] = true;
-  }
+  std::vector<int> uses(n + T, 0);
+  for (auto &t : p.temps) ++uses[t.first], ++uses[t.second];
   for (auto &r : p.rows)
+    for (int x : r) ++uses[x];
+  B.node.assign(n + T, {});
+  std::vector<bool> fused(n + T, false);
+  for (int t = 0; t < T; ++t) B.node[n + t] = {p.temps[t].first, p.temps[t].second};
+  auto fusable = [&](int c) { return c >= n && uses[c] == 1 && !fused[c] && B.node[c].size() == 2; };
+  for (int t = 0; t < T; ++t) {
+    auto &o = B.node[n + t];
+    for (size_t i = 0; i < o.size() && o.size() < 3; ++i)
+      if (fusable(o[i])) {
+        const int c = o[i];
+        fused[c] = true;
+        o.erase(o.begin() + i);
+        o.insert(o.end(), B.node[c].begin(), B.node[c].end());
+        B.node[c].clear();
+        break;
+      }
+  }
+  for (auto &r : p.rows) {
+    std::vector<int> e;
     for (int x : r)
-      if (x < n) used[x] = true;
-  std::printf("    {\n");
-  for (int g = 0; g < n / 4; ++g)
-    if (used[4 * g] || used[4 * g + 1] || used[4 * g + 2] || used[4 * g + 3])
-      std::printf("      const auto g%d = IN4(%d);\n", g, 4 * p0 + g);
-  auto nm = [&](int id) {
-    return id < n ? "g" + std::to_string(id / 4) + "[" + std::to_string(id % 4) + "]" : "t" + std::to_string(id);
+      if (fusable(x)) {
+        fused[x] = true;
+        e.insert(e.end(), B.node[x].begin(), B.node[x].end());
+        B.node[x].clear();
+      } else {
+        e.push_back(x);
+      }
+    B.rows.push_back(e);
+  }
+  B.group_used.assign(n / 4, false);
+  auto mark = [&](int x) {
+    if (x < n) B.group_used[x / 4] = true;
   };
-  // row o is ready once its largest temp id exists
+  for (int t = 0; t < T; ++t)
+    for (int x : B.node[n + t]) mark(x);
+  for (auto &r : B.rows)
+    for (int x : r) mark(x);
+  return B;
+}
+
+static void emit_loads(const Block &B, int bi) {
+  for (int g = 0; g < B.n / 4; ++g)
+    if (B.group_used[g]) std::printf("    const auto g%d_%d = IN4(%d);\n", bi, g, 4 * B.p0 + g);
+}
+
+// Emit a block's XORs; acc[] accumulates (first block: assigns).  Nodes are
+// emitted in creation order and every output row is folded in as soon as its
+// operands exist, so temps die early and register pressure stays bounded.
+static size_t emit_compute(const Block &B, int bi, bool first) {
+  const int n = B.n, T = (int)B.node.size() - n;
+  auto nm = [&](int id) {
+    return id < n ? "g" + std::to_string(bi) + "_" + std::to_string(id / 4) + "[" + std::to_string(id % 4) + "]"
+                  : "t" + std::to_string(bi) + "_" + std::to_string(id);
+  };
   std::vector<std::vector<int>> ready_at(T + 1);
-  for (size_t o = 0; o < p.rows.size(); ++o) {
+  for (size_t o = 0; o < B.rows.size(); ++o) {
     int mx = -1;
-    for (int x : p.rows[o])
+    for (int x : B.rows[o])
       if (x >= n) mx = std::max(mx, x - n);
     ready_at[mx + 1].push_back((int)o);
   }
-  size_t ops = T;
+  size_t ops = 0;
   auto fold = [&](int o) {
-    const auto &r = p.rows[o];
+    const auto &r = B.rows[o];
     if (r.empty()) {
-      if (first) std::printf("      acc[%d] = 0u;\n", o);
+      if (first) std::printf("    acc[%d] = 0u;\n", o);
       return;
     }
     std::string acc;
@@ -89,7 +139,6 @@ static size_t emit_block(const xorgen::XorProgram &p, int p0, bool first) {
     } else {
       acc = "acc[" + std::to_string(o) + "]";
     }
-    // v_bitop3_b32 (0x96) is a 3-input XOR on gfx950
     while (i < r.size()) {
       if (i + 1 < r.size()) {
         acc = "xor3(" + acc + ", " + nm(r[i]) + ", " + nm(r[i + 1]) + ")";
@@ -100,45 +149,69 @@ static size_t emit_block(const xorgen::XorProgram &p, int p0, bool first) {
       }
       ++ops;
     }
-    std::printf("      acc[%d] = %s;\n", o, acc.c_str());
+    std::printf("    acc[%d] = %s;\n", o, acc.c_str());
   };
   for (int o : ready_at[0]) fold(o);
   for (int t = 0; t < T; ++t) {
-    std::printf("      const uint32_t t%d = %s ^ %s;\n", n + t, nm(p.temps[t].first).c_str(),
-                nm(p.temps[t].second).c_str());
-    for (int o : ready_at[t + 1]) fold(o);
+    const auto &o = B.node[n + t];
+    if (o.size() == 2) {
+      std::printf("    const uint32_t %s = %s ^ %s;\n", nm(n + t).c_str(), nm(o[0]).c_str(), nm(o[1]).c_str());
+      ++ops;
+    } else if (o.size() == 3) {
+      std::printf("    const uint32_t %s = xor3(%s, %s, %s);\n", nm(n + t).c_str(), nm(o[0]).c_str(),
+                  nm(o[1]).c_str(), nm(o[2]).c_str());
+      ++ops;
+    }
+    for (int r : ready_at[t + 1]) fold(r);
   }
-  std::printf("    }\n");
   return ops;
 }
 
-// One wave's program: rows [r0, r0 + nr) of M (R x C), points blocked by `pb`.
-static size_t emit_program(const char *name, const std::vector<uint32_t> &M, int C, int r0, int nr, int pb) {
+// All bit-rows of y = M x for M (R x C field constants): row 16 m + i is the
+// set of input planes 16 j + b with bit i of M[m][j] * x^b set.
+static std::vector<std::vector<int>> all_bitrows(const std::vector<uint32_t> &M, int R, int C) {
+  return bitrows(M, R, C, 0, R);
+}
+
+// One wave's program: bit-rows [row0, row0 + nrows) of the map, points
+// blocked by `pb`.  The LDS reads of block b + 1 are issued before the XORs of
+// block b so their latency hides under them.
+static size_t emit_program(const char *name, const std::vector<std::vector<int>> &rows, int C, int row0, int nrows,
+                           int pb) {
   std::printf("  template <typename In>\n  __device__ __forceinline__ static void %s(const In &IN4, uint32_t (&acc)[%d]) {\n",
-              name, 16 * nr);
-  size_t ops = 0;
+              name, nrows);
+  std::vector<Block> blocks;
   for (int c0 = 0; c0 < C; c0 += pb) {
     const int cb = std::min(pb, C - c0);
-    std::vector<uint32_t> sub((size_t)nr * cb);
-    for (int m = 0; m < nr; ++m)
-      for (int j = 0; j < cb; ++j) sub[(size_t)m * cb + j] = M[(size_t)(r0 + m) * C + c0 + j];
-    ops += emit_block(xorgen::paar(16 * cb, bitrows(sub, nr, cb, 0, nr)), c0, c0 == 0);
+    std::vector<std::vector<int>> sub(nrows);
+    for (int r = 0; r < nrows; ++r)
+      for (int x : rows[row0 + r])
+        if (x >= 16 * c0 && x < 16 * (c0 + cb)) sub[r].push_back(x - 16 * c0);
+    blocks.push_back(make_block(xorgen::paar(16 * cb, sub), c0));
+  }
+  size_t ops = 0;
+  emit_loads(blocks[0], 0);
+  for (size_t b = 0; b < blocks.size(); ++b) {
+    if (b + 1 < blocks.size()) emit_loads(blocks[b + 1], (int)b + 1);
+    ops += emit_compute(blocks[b], (int)b, b == 0);
+    // keep the scheduler from hoisting later blocks' LDS reads (and their
+    // registers) above this block
+    std::printf("    VDS_SCHED_FENCE();\n");
   }
   std::printf("  }\n");
+  std::fprintf(stderr, "  %s: %zu ops\n", name, ops);
   return ops;
 }
 
 int main(int argc, char **argv) {
-  if (argc != 3 && argc != 5) {
-    std::fprintf(stderr, "usage: %s K N [syndrome_block interp_block]\n", argv[0]);
+  if (argc != 6) {
+    std::fprintf(stderr, "usage: %s K N WAVES syndrome_block interp_block\n", argv[0]);
     return 2;
   }
-  const int K = std::atoi(argv[1]), N = std::atoi(argv[2]), M = N - K;
-  const int syn_pb = argc == 5 ? std::atoi(argv[3]) : 4;
-  const int int_pb = argc == 5 ? std::atoi(argv[4]) : 1;
-  const int waves = K / 4;
-  if (K % 4 || M != waves) {
-    std::fprintf(stderr, "layout needs K %% 4 == 0 and N - K == K / 4\n");
+  const int K = std::atoi(argv[1]), N = std::atoi(argv[2]), M = N - K, waves = std::atoi(argv[3]);
+  const int syn_pb = std::atoi(argv[4]), int_pb = std::atoi(argv[5]);
+  if ((16 * M) % waves || (16 * K) % waves) {
+    std::fprintf(stderr, "16 (N - K) and 16 K must split evenly over the waves\\n");
     return 2;
   }
   // syndrome matrix W (M x N)
@@ -155,12 +228,14 @@ int main(int argc, char **argv) {
   for (int i = 0; i < K; ++i) nodes[i] = (uint16_t)i;
   if (vds_ec_inverse16(K, nodes.data(), inv.data()) != VDS_EC_OK) return 1;
   std::vector<uint32_t> Vi(inv.begin(), inv.end());
+  const int syn_rows = 16 * M / waves, int_rows = 16 * K / waves;
 
-  std::printf("// GENERATED by tools/xorgen/gen_restore %d %d -- do not edit.\n", K, N);
-  std::printf("// Syndrome and fixed-interpolation XOR programs for k_restore_syn<%d,%d>\n", K, N);
+  std::printf("// GENERATED by tools/xorgen/gen_restore %d %d %d %d %d -- do not edit.\n", K, N, waves, syn_pb, int_pb);
+  std::printf("// Syndrome and fixed-interpolation XOR programs for k_restore_syn<%d,%d> with %d waves\n", K, N, waves);
   std::printf("// (points blocked by %d / %d; IN4(g) = planes 4g..4g+3, plane = 16 point + bit).\n", syn_pb, int_pb);
-  std::printf("template <> struct RestorePrograms<%d, %d> {\n", K, N);
-  std::printf("  static constexpr int kWaves = %d;\n", waves);
+  std::printf("template <> struct RestorePrograms<%d, %d, %d> {\n", K, N, waves);
+  std::printf("  static constexpr int kSynRows = %d;  // syndrome bit-rows per wave (wave w: rows %d w ..)\n", syn_rows, syn_rows);
+  std::printf("  static constexpr int kIntRows = %d;  // object bit-rows per wave (cells %d w ..)\n", int_rows, int_rows / 16);
   // the syndrome weights v_a a^j, for the host-side solve (row j, column a)
   std::printf("  static constexpr uint16_t kSyndromeW[%d][%d] = {\n", M, N);
   for (int j = 0; j < M; ++j) {
@@ -169,19 +244,27 @@ int main(int argc, char **argv) {
     std::printf("},\n");
   }
   std::printf("  };\n");
+  const auto wrows = all_bitrows(W, M, N), vrows = all_bitrows(Vi, K, K);
   size_t total = 0;
-  for (int w = 0; w < waves; ++w) {  // wave w: syndrome S_w (16 planes, N points)
+  for (int w = 0; w < waves; ++w) {
     char name[64];
     std::snprintf(name, sizeof name, "syndrome%d", w);
-    total += emit_program(name, W, N, w, 1, syn_pb);
+    total += emit_program(name, wrows, N, syn_rows * w, syn_rows, syn_pb);
   }
-  for (int w = 0; w < waves; ++w) {  // wave w: cells 4w..4w+3 (64 planes, points 0..K-1)
+  for (int w = 0; w < waves; ++w) {
     char name[64];
     std::snprintf(name, sizeof name, "interp%d", w);
-    total += emit_program(name, Vi, K, 4 * w, 4, int_pb);
+    total += emit_program(name, vrows, K, int_rows * w, int_rows, int_pb);
+  }
+  for (const char *kind : {"syndrome", "interp"}) {
+    std::printf("  template <typename In>\n  __device__ __forceinline__ static void %s(int w, const In &IN4, uint32_t (&acc)[%d]) {\n",
+                kind, kind[0] == 's' ? syn_rows : int_rows);
+    std::printf("    switch (w) {\n");
+    for (int w = 0; w < waves; ++w) std::printf("      case %d: %s%d(IN4, acc); break;\n", w, kind, w);
+    std::printf("      default: break;\n    }\n  }\n");
   }
   std::printf("  static constexpr int kXorOps = %zu;\n", total);
   std::printf("};\n");
-  std::fprintf(stderr, "K=%d N=%d: %zu XOR ops per 32 stripes\n", K, N, total);
+  std::fprintf(stderr, "K=%d N=%d waves=%d: %zu XOR instructions per 32 stripes\n", K, N, waves, total);
   return 0;
 }

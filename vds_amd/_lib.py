@@ -10,7 +10,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libvds_ec.so")
+LIB_PATH = os.environ.get("VDS_EC_LIB") or os.path.join(HERE, "libvds_ec.so")
 
 OK = 0
 EINVAL = -1

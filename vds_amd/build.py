@@ -31,16 +31,24 @@ def _stale() -> bool:
         return True
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "vds_ec.h")]
+    gen = os.path.join(CSRC, "generated")
+    if os.path.isdir(gen):
+        deps += [os.path.join(gen, f) for f in os.listdir(gen)]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, out: str | None = None,
+          defines: tuple[str, ...] = ()) -> str:
+    """Build the library (default: in-tree libvds_ec.so, rebuilt when stale).
+    `out` + `defines` build a variant (e.g. -DVDS_SYN_PREFETCH=0) for A/B
+    measurements; the variant is loaded with VDS_EC_LIB=<path>."""
+    lib = out or LIB
+    if out is None and not force and not _stale():
         return LIB
     objs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-c",
+        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + (".variant.o" if out else ".o"))
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-c", *defines,
                "-I", os.path.join(ROOT, "include"), os.path.join(CSRC, src), "-o", obj]
         if src.endswith(".cpp"):
             cmd[1:1] = ["-x", "hip"]
@@ -48,13 +56,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs +
                    ["-lpthread"], check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

@@ -160,21 +160,53 @@ VDS_INLINE void plane_mac_rt(Plane16 (&acc)[NS], Plane16 y, const uint32_t (&c)[
 
 // One butterfly round of the bit transpose for a power-of-two shift J < 8:
 // swaps (row k, bits with J set) <-> (row k+J, bits with J clear).
+// Masks of the j = 4, 2, 1 transpose rounds.  On the device they live in
+// VGPRs: a v_bitop3_b32 whose operands are all VGPRs issues at the rate of a
+// 2-input XOR, while one reading an SGPR (or v_bfi_b32) issues at ~0.6 of it
+// (tools/ubench/valu_latency.hip).  The asm is not volatile, so the movs are
+// CSE'd and hoisted out of the tile loops.
+struct BitMasks {
+  uint32_t m4, m2, m1;
+};
+
+VDS_INLINE BitMasks bit_masks() {
+  BitMasks m;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("v_mov_b32 %0, %1" : "=v"(m.m4) : "i"(0x0F0F0F0F));
+  asm("v_mov_b32 %0, %1" : "=v"(m.m2) : "i"(0x33333333));
+  asm("v_mov_b32 %0, %1" : "=v"(m.m1) : "i"(0x55555555));
+#else
+  m.m4 = 0x0F0F0F0Fu;
+  m.m2 = 0x33333333u;
+  m.m1 = 0x55555555u;
+#endif
+  return m;
+}
+
+// (m & a) | (~m & b): truth table over S0=0xF0 (m), S1=0xCC (a), S2=0xAA (b)
+VDS_INLINE uint32_t bit_select(uint32_t m, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);
+#else
+  return (m & a) | (~m & b);
+#endif
+}
+
 template <int J, int ROWS, typename Arr>
-VDS_INLINE void transpose_round(Arr &A) {
-  constexpr uint32_t m = (J == 4) ? 0x0F0F0F0Fu : (J == 2) ? 0x33333333u : 0x55555555u;
+VDS_INLINE void transpose_round(Arr &A, const BitMasks &bm) {
+  const uint32_t m = (J == 4) ? bm.m4 : (J == 2) ? bm.m2 : bm.m1;
 #pragma unroll
   for (int k0 = 0; k0 < ROWS; k0 += 2 * J)
 #pragma unroll
     for (int k = k0; k < k0 + J; ++k) {
       const uint32_t a = A[k], b = A[k + J];
-      A[k] = (a & m) | ((b << J) & ~m);
-      A[k + J] = ((a >> J) & m) | (b & ~m);
+      A[k] = bit_select(m, a, b << J);
+      A[k + J] = bit_select(m, a >> J, b);
     }
 }
 
 // 32x32 bit transpose in place: afterwards A[p] bit i == before A[i] bit p.
-VDS_INLINE void transpose32(uint32_t (&A)[32]) {
+VDS_INLINE void transpose32(uint32_t (&A)[32], const BitMasks &bm = bit_masks()) {
   // j = 16: swap (row k, bits 16..31) <-> (row k+16, bits 0..15)
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -202,14 +234,14 @@ VDS_INLINE void transpose32(uint32_t (&A)[32]) {
 #endif
     }
   // j = 4, 2, 1 : bitfield inserts
-  transpose_round<4, 32>(A);
-  transpose_round<2, 32>(A);
-  transpose_round<1, 32>(A);
+  transpose_round<4, 32>(A, bm);
+  transpose_round<2, 32>(A, bm);
+  transpose_round<1, 32>(A, bm);
 }
 
 // Two independent 16x16 bit transposes held in the low / high halves of 16
 // words: afterwards A[q] bit (16h + j) == before A[j] bit (16h + q).
-VDS_INLINE void transpose16x2(uint32_t (&A)[16]) {
+VDS_INLINE void transpose16x2(uint32_t (&A)[16], const BitMasks &bm = bit_masks()) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const uint32_t a = A[k], b = A[k + 8];
@@ -221,9 +253,9 @@ VDS_INLINE void transpose16x2(uint32_t (&A)[16]) {
     A[k + 8] = ((a >> 8) & 0x00FF00FFu) | (b & 0xFF00FF00u);
 #endif
   }
-  transpose_round<4, 16>(A);
-  transpose_round<2, 16>(A);
-  transpose_round<1, 16>(A);
+  transpose_round<4, 16>(A, bm);
+  transpose_round<2, 16>(A, bm);
+  transpose_round<1, 16>(A, bm);
 }
 
 }  // namespace vds_ec

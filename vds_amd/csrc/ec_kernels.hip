@@ -448,48 +448,48 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
 
 // ============================================ erasure-pattern-independent restore
 
-template <int K, int N> struct RestorePrograms;
-#include "generated/restore_16_20.inc"
+template <int K, int N, int WV> struct RestorePrograms;
+#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#ifdef VDS_SYN_INC  // A/B builds of alternative generated programs
+#include VDS_SYN_INC
+#else
+#include "generated/restore_16_20_w4.inc"
+#endif
+#undef VDS_SCHED_FENCE
 
-template <int K, int N>
+// k_restore_syn<K, N, WV>: one 2048-stripe tile per workgroup of WV waves.
+template <int K, int N, int WV>
 struct SynShape {
-  static constexpr int kWaves = K / 4;
-  static constexpr int kThreads = 64 * kWaves;
+  static constexpr int kWaves = WV;
+  static constexpr int kThreads = 64 * WV;
   static constexpr int kM = N - K;
+  static constexpr int kLoadPer = K / WV;          // survivors loaded per wave
+  using P = RestorePrograms<K, N, WV>;
+  static constexpr int kSynRows = P::kSynRows;     // syndrome bit-rows per wave
+  static constexpr int kCells = P::kIntRows / 16;  // object cells per wave
   // group-major LDS: plane p = 16 point + bit lives in group p / 4; the four
   // planes of a group are one 16-byte word per lane, so every access is a
-  // conflict-free ds_{read,write}_b128 (word (p/4)*256 + lane*4 + p%4)
+  // conflict-free ds_{read,write}_b128 (byte (p/4)*1024 + lane*16 + 4*(p%4))
   static constexpr int kLdsBytes = N * 16 * 64 * 4;
-  static_assert(kM == kWaves, "one syndrome / one erased point per wave");
+  static constexpr int kWavesPerSimd = (160 * 1024 / kLdsBytes) * WV / 4;
+  static_assert(K % WV == 0 && kM <= WV, "survivor loads and erased slots must map onto waves");
+  static_assert(kSynRows % 4 == 0 && (kCells == 2 || kCells == 4), "row split must be b128 / word-group aligned");
 };
 
 typedef __attribute__((address_space(3))) volatile u32x4 lds_v4;
+typedef __attribute__((address_space(3))) char lds_char;
 
-// The 16 planes of point `pt` as four b128 LDS accesses.
-__device__ __forceinline__ void syn_put_point(uint32_t *lds, int lane, int pt, const uint32_t (&v)[16]) {
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    lds_v4 *d = (lds_v4 *)(lds + (4 * pt + g) * 256 + 4 * lane);
-    *d = u32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
-  }
-}
-
-__device__ __forceinline__ void syn_get_point(const uint32_t *lds, int lane, int pt, uint32_t (&v)[16]) {
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const u32x4 x = *(const lds_v4 *)(lds + (4 * pt + g) * 256 + 4 * lane);
-    v[4 * g] = x[0];
-    v[4 * g + 1] = x[1];
-    v[4 * g + 2] = x[2];
-    v[4 * g + 3] = x[3];
-  }
-}
+// Diagnostic build switch (wrong results; timing only): every wave runs wave
+// 1's programs, to measure what the per-wave code footprint costs.
+#ifndef VDS_SYN_SAME_CODE
+#define VDS_SYN_SAME_CODE 0
+#endif
+constexpr bool kSynSameCode = VDS_SYN_SAME_CODE;
 
 // Group g of the plane-major LDS as seen by one lane.  ds_read_b128 carries a
 // 16-bit immediate offset, so groups past 64 KiB (points >= 16) are addressed
 // from a second base register; the base is laundered through an empty asm so
 // the compiler does not fold it back into one address register per group.
-typedef __attribute__((address_space(3))) char lds_char;
 struct SynLds {
   lds_char *base;
   uint32_t lo;  // 16 * lane
@@ -498,152 +498,161 @@ struct SynLds {
     if (g < 64) return *(lds_v4 *)(base + lo + g * 1024);
     return *(lds_v4 *)(base + hi + (g - 64) * 1024);
   }
+  __device__ __forceinline__ void put(int g, u32x4 v) const {
+    *(lds_v4 *)(base + lo + g * 1024) = v;  // runtime g: one address add
+  }
 };
 
-template <int K, int N, int W>
-__device__ __forceinline__ void syn_dispatch_syndrome(int wave, const SynLds &in4, uint32_t (&out)[16]) {
-  if constexpr (W < SynShape<K, N>::kWaves) {
-    if (wave == W) {
-      if constexpr (W == 0) RestorePrograms<K, N>::syndrome0(in4, out);
-      else if constexpr (W == 1) RestorePrograms<K, N>::syndrome1(in4, out);
-      else if constexpr (W == 2) RestorePrograms<K, N>::syndrome2(in4, out);
-      else if constexpr (W == 3) RestorePrograms<K, N>::syndrome3(in4, out);
-    } else {
-      syn_dispatch_syndrome<K, N, W + 1>(wave, in4, out);
-    }
-  }
+__device__ __forceinline__ void syn_put_point(const SynLds &L, int pt, const uint32_t (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) L.put(4 * pt + g, u32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]});
 }
 
-template <int K, int N, int W>
-__device__ __forceinline__ void syn_dispatch_interp(int wave, const SynLds &in4, uint32_t (&out)[64]) {
-  if constexpr (W < SynShape<K, N>::kWaves) {
-    if (wave == W) {
-      if constexpr (W == 0) RestorePrograms<K, N>::interp0(in4, out);
-      else if constexpr (W == 1) RestorePrograms<K, N>::interp1(in4, out);
-      else if constexpr (W == 2) RestorePrograms<K, N>::interp2(in4, out);
-      else if constexpr (W == 3) RestorePrograms<K, N>::interp3(in4, out);
-    } else {
-      syn_dispatch_interp<K, N, W + 1>(wave, in4, out);
-    }
+__device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const u32x4 x = *(lds_v4 *)(L.base + L.lo + (4 * pt + g) * 1024);
+    v[4 * g] = x[0];
+    v[4 * g + 1] = x[1];
+    v[4 * g + 2] = x[2];
+    v[4 * g + 3] = x[3];
   }
 }
 
 // Restore of an object from any K of its N replicas without a per-pattern
-// K x K inverse.  Wave w: loads survivors 4w..4w+3 into their points' planes;
-// computes syndrome S_w over all N points (erased points read as zero); solves
-// its erased point c_{e_w} = sum_j R[w][j] S_j (the only runtime-coefficient
-// arithmetic, M multiplies); then interpolates cells 4w..4w+3 from the fixed
-// points 0..K-1 and stores them big-endian.  See tools/xorgen/gen_restore.cpp.
-template <int K, int N>
-__global__ __launch_bounds__((SynShape<K, N>::kThreads), 2) void k_restore_syn(SynRestoreArgs a) {
-  using S = SynShape<K, N>;
+// K x K inverse (tools/xorgen/gen_restore.cpp).  Per tile, wave w:
+//  1. loads survivors kLoadPer*w.. into their points' planes (waves < M also
+//     zero one erased point);
+//  2. computes syndrome bit-rows kSynRows*w.. over all N points (erased
+//     points read as zero) and parks them in the erased slots;
+//  3. (waves < M) recovers erased point e_w = sum_j R[w][j] S_j by Horner
+//     over the coefficient bits -- the only runtime-coefficient arithmetic;
+//  4. interpolates cells kCells*w.. from the fixed points 0..K-1 and stores
+//     them big-endian.
+template <int K, int N, int WV>
+__global__ __launch_bounds__((SynShape<K, N, WV>::kThreads), (SynShape<K, N, WV>::kWavesPerSimd))
+void k_restore_syn(SynRestoreArgs a) {
+  using S = SynShape<K, N, WV>;
+  using P = typename S::P;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  constexpr int kPer = K / S::kWaves;  // survivors loaded per wave (4)
+  const BitMasks bm = bit_masks();
+  SynLds L;
+  L.base = (lds_char *)lds;
+  L.lo = 16u * lane;
+  L.hi = 16u * lane + 65536u;
+  asm volatile("" : "+v"(L.hi));
+  const int my_erased = wave < S::kM ? a.erased[wave] : 0;
 
-  u32x4 Q[kPer][4];
-  auto load = [&](uint32_t tile) {
-    const uint32_t o = tile / a.tiles_per_obj;
-    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
+  // survivor staging: the next tile's loads are issued after the syndrome
+  // programs and land while the recovery and interpolation run
+  u32x4 Q[S::kLoadPer][4];
+  auto load = [&](uint32_t t) {
+    const uint32_t ob = t / a.tiles_per_obj;
+    const uint64_t st0 = (uint64_t)(t % a.tiles_per_obj) * kTileStripes;
 #pragma unroll
-    for (int s = 0; s < kPer; ++s) {
-      const uint8_t *src = a.chunks[wave * kPer + s] + (uint64_t)o * a.chunk_stride + 2 * stripe0 + 16 * lane;
+    for (int s = 0; s < S::kLoadPer; ++s) {
+      const uint8_t *src = a.chunks[wave * S::kLoadPer + s] + (uint64_t)ob * a.chunk_stride + 2 * st0 + 16 * lane;
 #pragma unroll
       for (int q = 0; q < 4; ++q) Q[s][q] = *reinterpret_cast<const u32x4 *>(src + 1024 * q);
     }
   };
-  SynLds in4;
-  in4.base = (lds_char *)lds;
-  in4.lo = 16u * lane;
-  in4.hi = 16u * lane + 65536u;
-  asm volatile("" : "+v"(in4.hi));
-  uint32_t tile = blockIdx.x;
-  if (tile < a.total_tiles) load(tile);
-  const int my_erased = a.erased[wave];
-  for (; tile < a.total_tiles; tile += gridDim.x) {
-    // ---- 1. survivors -> planes of their points; this wave's erased point -> 0
-#pragma unroll
-    for (int s = 0; s < kPer; ++s) {
-      uint32_t W[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int d = 0; d < 4; ++d) W[4 * q + d] = Q[s][q][d];
-      transpose16x2(W);  // W[x] = plane of cell bit x^8
-      uint32_t P[16];
-#pragma unroll
-      for (int b = 0; b < 16; ++b) P[b] = W[b ^ 8];
-      syn_put_point(lds, lane, a.point[wave * kPer + s], P);
-    }
-    {
-      uint32_t Z[16];
-#pragma unroll
-      for (int b = 0; b < 16; ++b) Z[b] = 0u;
-      syn_put_point(lds, lane, my_erased, Z);
-    }
-    __syncthreads();
-    // ---- 2. syndrome S_wave over all N points
-    uint32_t syn[16];
-    syn_dispatch_syndrome<K, N, 0>(wave, in4, syn);
-    // prefetch the next tile (issued after the syndrome, whose block temps
-    // would otherwise share the register file with the 64 staging registers)
-    const uint32_t next = tile + gridDim.x;
-    if (next < a.total_tiles) load(next);
-    __syncthreads();  // every wave is done reading the zeroed erased planes
-    syn_put_point(lds, lane, my_erased, syn);  // park S_wave in the erased slot
-    __syncthreads();
-    // ---- 3. c_e = sum_j R[wave][j] S_j (e = this wave's erased point), by
-    // Horner over the 16 coefficient bits: ce = ce * x, then add the S_j whose
-    // coefficient has that bit set.  The selections are wave-uniform bytes
-    // (host-precomputed), so the adds are scalar branches over plain XORs.
-    Plane16 sy[S::kM];
-#pragma unroll
-    for (int j = 0; j < S::kM; ++j) syn_get_point(lds, lane, a.erased[j], sy[j].p);
-    __syncthreads();  // every wave has read all syndromes
-    Plane16 ce = plane_zero();
-#pragma unroll
-    for (int b = 15; b >= 0; --b) {
-      if (b != 15) ce = plane_mulx(ce);
-      const uint32_t sel = (a.solve_sel[wave][b >> 2] >> (8 * (b & 3))) & 0xFFu;
-#pragma unroll
-      for (int j = 0; j < S::kM; j += 2) {
-        const uint32_t two = (sel >> j) & 3u;
-        if (two == 1u)
-          ce = plane_xor(ce, sy[j]);
-        else if (two == 2u)
-          ce = plane_xor(ce, sy[j + 1]);
-        else if (two == 3u)
-          ce = plane_xor3(ce, sy[j], sy[j + 1]);
-      }
-    }
-    syn_put_point(lds, lane, my_erased, ce.p);
-    __syncthreads();
-    // ---- 4. fixed interpolation from points 0..K-1: cells 4 wave .. 4 wave + 3
-    uint32_t cells[64];
-    syn_dispatch_interp<K, N, 0>(wave, in4, cells);
-    // ---- 5. back to big-endian cells: word groups 2 wave, 2 wave + 1 (cells
-    // 4 wave .. 4 wave + 3, 8 contiguous bytes of every stripe) as 8-byte stores
+  if (blockIdx.x < a.total_tiles) load(blockIdx.x);
+  for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
     const uint32_t o = tile / a.tiles_per_obj;
     const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
-    uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
-    uint32_t rows[2][32];
+    // ---- 1. survivors -> planes of their points; waves < M zero one erased point
+    {
+      if (wave < S::kM) {
+        const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < 4; ++g) L.put(4 * my_erased + g, z);
+      }
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int s = 0; s < S::kLoadPer; ++s) {
+        uint32_t W[16];
 #pragma unroll
-        for (int jb = 0; jb < 16; ++jb) rows[g][16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
-      transpose32(rows[g]);
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) W[4 * q + d] = Q[s][q][d];
+        transpose16x2(W, bm);  // W[x] = plane of cell bit x^8
+        uint32_t Pl[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) Pl[b] = W[b ^ 8];
+        syn_put_point(L, a.point[wave * S::kLoadPer + s], Pl);
+      }
     }
+    __syncthreads();
+    // ---- 2. syndrome bit-rows of this wave, parked in the erased slots
+    {
+      uint32_t syn[S::kSynRows];
+      P::syndrome(kSynSameCode ? 1 : wave, L, syn);
+      if (tile + gridDim.x < a.total_tiles) load(tile + gridDim.x);
+      __syncthreads();  // every wave is done reading the zeroed erased planes
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint8_t *base = dst + (stripe0 + 8u * lane + 512u * q) * (2 * K) + 8 * wave;
+      for (int r = 0; r < S::kSynRows; r += 4) {
+        const int q = S::kSynRows * wave + r;  // syndrome q / 16, planes q % 16 ..
+        L.put(4 * a.erased[q >> 4] + ((q & 15) >> 2), u32x4{syn[r], syn[r + 1], syn[r + 2], syn[r + 3]});
+      }
+    }
+    __syncthreads();
+    // ---- 3. c_e = sum_j R[w][j] S_j for e = erased[w], w < M: Horner over the
+    // 16 coefficient bits (ce = ce * x, then add the S_j whose coefficient has
+    // that bit); the selections are wave-uniform bytes, the adds plain XORs
+    if (wave < S::kM) {
+      Plane16 sy[S::kM];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int slot = 8 * q + e;
-        const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
-        *reinterpret_cast<uint2 *>(base + e * (2 * K)) = make_uint2(rows[0][pi], rows[1][pi]);
+      for (int j = 0; j < S::kM; ++j) syn_get_point(L, a.erased[j], sy[j].p);
+      Plane16 ce = plane_zero();
+#pragma unroll
+      for (int b = 15; b >= 0; --b) {
+        if (b != 15) ce = plane_mulx(ce);
+        const uint32_t sel = (a.solve_sel[wave][b >> 2] >> (8 * (b & 3))) & 0xFFu;
+#pragma unroll
+        for (int j = 0; j < S::kM; j += 2) {
+          const uint32_t two = (sel >> j) & 3u;
+          if (two == 1u)
+            ce = plane_xor(ce, sy[j]);
+          else if (two == 2u)
+            ce = plane_xor(ce, sy[j + 1]);
+          else if (two == 3u)
+            ce = plane_xor3(ce, sy[j], sy[j + 1]);
+        }
+      }
+      __syncthreads();  // every recovering wave has read all syndromes
+      syn_put_point(L, my_erased, ce.p);
+    } else {
+      __syncthreads();
+    }
+    __syncthreads();
+    // ---- 4. fixed interpolation from points 0..K-1, then big-endian stores
+    {
+      uint32_t cells[16 * S::kCells];
+      P::interp(kSynSameCode ? 1 : wave, L, cells);
+      uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
+      constexpr int kGroups = S::kCells / 2;  // word groups (2 cells) per wave
+      uint32_t rows[kGroups][32];
+#pragma unroll
+      for (int g = 0; g < kGroups; ++g) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int jb = 0; jb < 16; ++jb) rows[g][16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
+        transpose32(rows[g], bm);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint8_t *base = dst + (stripe0 + 8u * lane + 512u * q) * (2 * K) + 4 * kGroups * wave;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int slot = 8 * q + e;
+          const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+          if constexpr (kGroups == 2)
+            *reinterpret_cast<uint2 *>(base + e * (2 * K)) = make_uint2(rows[0][pi], rows[1][pi]);
+          else
+            *reinterpret_cast<uint32_t *>(base + e * (2 * K)) = rows[0][pi];
+        }
       }
     }
     __syncthreads();
@@ -757,17 +766,19 @@ hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t
 
 bool has_restore_syn(uint32_t k, uint32_t n) { return k == 16 && n == 20; }
 
+constexpr int kSynWaves16 = 4;
+
 const uint16_t *restore_syn_weights(uint32_t k, uint32_t n) {
-  if (k == 16 && n == 20) return &RestorePrograms<16, 20>::kSyndromeW[0][0];
+  if (k == 16 && n == 20) return &RestorePrograms<16, 20, kSynWaves16>::kSyndromeW[0][0];
   return nullptr;
 }
 
-template <int K, int N>
+template <int K, int N, int WV>
 static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) {
-  using S = SynShape<K, N>;
+  using S = SynShape<K, N, WV>;
   static bool configured = false;
   if (!configured) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_restore_syn<K, N>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_restore_syn<K, N, WV>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, S::kLdsBytes);
     if (e != hipSuccess) return e;
     configured = true;
@@ -776,12 +787,12 @@ static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) 
   int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
   if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_restore_syn<K, N>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  hipLaunchKernelGGL((k_restore_syn<K, N, WV>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s) {
-  if (k == 16 && n == 20) return launch_restore_syn_kn<16, 20>(a, s);
+  if (k == 16 && n == 20) return launch_restore_syn_kn<16, 20, kSynWaves16>(a, s);
   return hipErrorNotSupported;
 }
 

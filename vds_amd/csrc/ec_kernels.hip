@@ -632,26 +632,59 @@ void k_restore_syn(SynRestoreArgs a) {
       P::interp(kSynSameCode ? 1 : wave, L, cells);
       uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
       constexpr int kGroups = S::kCells / 2;  // word groups (2 cells) per wave
-      uint32_t rows[kGroups][32];
+      if constexpr (kGroups == 2) {
+        // Stage the tile's output in LDS (the planes are dead once every wave
+        // has interpolated), stripe-major with 16 bytes of padding after every
+        // 16 stripes: the writes of one instruction then hit distinct banks,
+        // and the copy-out is 16 contiguous bytes per lane, so every HBM
+        // write is a whole 1 KiB wave-instruction (no partial lines).  One
+        // word group at a time keeps 32, not 64, transposed rows live.
+        static_assert(K == 16 && WV == 4 && 2048 * 32 + 128 * 16 <= S::kLdsBytes,
+                      "staging layout is for 32-byte stripes, 4 waves");
+        __syncthreads();
 #pragma unroll
-      for (int g = 0; g < kGroups; ++g) {
+        for (int g = 0; g < kGroups; ++g) {
+          uint32_t rows[32];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int jb = 0; jb < 16; ++jb) rows[16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
+          transpose32(rows, bm);
+          // slot 8q+e is stripe st = 8 lane + 512 q + e at byte st*32 + (st/16)*16,
+          // i.e. a per-lane base plus a compile-time offset
+          lds_char *w0 = L.base + 256u * lane + 16u * (lane >> 1) + 4u * (kGroups * wave + g);
+#pragma unroll
+          for (int slot = 0; slot < 32; ++slot) {
+            const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+            *(__attribute__((address_space(3))) uint32_t *)(w0 + (slot >> 3) * (16384 + 512) + (slot & 7) * 32) =
+                rows[pi];
+          }
+        }
+        __syncthreads();
+        // 16-byte chunk c = 64 (16 wave + i) + lane of the tile: stripe c/2, half c%2
+        const lds_char *r0 = L.base + 1056u * 16u * wave + 32u * (lane >> 1) + 16u * (lane >> 5) + 16u * (lane & 1);
+        uint8_t *g0 = dst + stripe0 * (2 * K) + 16384u * wave + 16u * lane;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const u32x4 v = *(lds_v4 *)(r0 + 1056 * i);
+          *reinterpret_cast<u32x4 *>(g0 + 1024 * i) = v;
+        }
+      } else {
+        uint32_t rows[1][32];
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int jb = 0; jb < 16; ++jb) rows[g][16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
-        transpose32(rows[g], bm);
-      }
+          for (int jb = 0; jb < 16; ++jb) rows[0][16 * h + jb] = cells[16 * h + (jb ^ 8)];
+        transpose32(rows[0], bm);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint8_t *base = dst + (stripe0 + 8u * lane + 512u * q) * (2 * K) + 4 * kGroups * wave;
+        for (int q = 0; q < 4; ++q) {
+          uint8_t *base = dst + (stripe0 + 8u * lane + 512u * q) * (2 * K) + 4 * wave;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int slot = 8 * q + e;
-          const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
-          if constexpr (kGroups == 2)
-            *reinterpret_cast<uint2 *>(base + e * (2 * K)) = make_uint2(rows[0][pi], rows[1][pi]);
-          else
+          for (int e = 0; e < 8; ++e) {
+            const int slot = 8 * q + e;
+            const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
             *reinterpret_cast<uint32_t *>(base + e * (2 * K)) = rows[0][pi];
+          }
         }
       }
     }

@@ -169,16 +169,20 @@ constexpr ReplicaPlan<N, WAVES, RPW> plan_replicas() {
   return p;
 }
 
-template <int K, int N, int RPW>
+template <int K, int N, int RPW, int WV>
 struct EncodeShape {
-  static constexpr int kWaves = (N + RPW - 1) / RPW;
+  static constexpr int kWaves = WV;
   static constexpr int kThreads = kWaves * 64;
   static constexpr int kWordGroups = K / 2;                 // dwords per stripe
   static constexpr int kGroupsPerWave = kWordGroups / kWaves;
   static constexpr int kSetWords = K * 16 + 4;              // planes per set + pad
   static constexpr int kLdsBytes = 64 * kSetWords * 4;
+  // waves per SIMD the register budget is sized for: 2 (256 VGPRs) unless
+  // two 8-wave workgroups fit a CU (4, i.e. 128 VGPRs)
+  static constexpr int kWavesPerSimd = (WV >= 8 && 2 * kLdsBytes <= 160 * 1024) ? 4 : 2;
   static constexpr ReplicaPlan<N, kWaves, RPW> kPlan = plan_replicas<N, kWaves, RPW>();
   static_assert(kWordGroups % kWaves == 0, "word groups must split evenly over waves");
+  static_assert(RPW * WV >= N, "every replica needs a wave");
   static_assert(K % 2 == 0, "fast path needs even k");
 };
 
@@ -202,26 +206,27 @@ __device__ __forceinline__ Plane16 lds_planes(const uint32_t *p) {
   return x;
 }
 
-// Transpose one replica's planes back to big-endian cells and store them:
-// lane l pairs with lane l^1 so every store is a 4-byte word of two adjacent
-// stripes' cells.
-__device__ __forceinline__ void store_replica(const Plane16 &acc, uint8_t *base, uint32_t sel) {
+// Transpose one replica's planes back to big-endian cells and store them.
+// After the transpose, word q of lane l holds the cells of stripes l + 64 q
+// (low half) and l + 1024 + 64 q (high half); each half goes out as a 2-byte
+// store (global_store_short / _d16_hi), so one wave-instruction writes 128
+// contiguous bytes and no cross-lane shuffle is needed.
+__device__ __forceinline__ void store_replica(const Plane16 &acc, uint8_t *base, const BitMasks &bm) {
   uint32_t rows[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) rows[j] = acc.p[j ^ 8];  // word bit j <-> cell bit j^8 (BE)
-  transpose16x2(rows);
+  transpose16x2(rows, bm);
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    // lane l^1 via DPP quad_perm [1,0,3,2] (no LDS permute)
-    const uint32_t nb = (uint32_t)__builtin_amdgcn_mov_dpp((int)rows[q], 0xB1, 0xF, 0xF, false);
-    *reinterpret_cast<uint32_t *>(base + 128 * q) = __builtin_amdgcn_perm(nb, rows[q], sel);
+    *reinterpret_cast<uint16_t *>(base + 128 * q) = (uint16_t)rows[q];
+    *reinterpret_cast<uint16_t *>(base + 2048 + 128 * q) = (uint16_t)(rows[q] >> 16);
   }
 }
 
-template <int K, int N, int RPW, int W>
+template <int K, int N, int RPW, int WV, int W>
 __device__ __forceinline__ void encode_wave_group(const uint32_t *set_planes, const FastEncodeArgs &a,
-                                                  uint64_t out_off, uint32_t sel) {
-  using S = EncodeShape<K, N, RPW>;
+                                                  uint64_t out_off, const BitMasks &bm) {
+  using S = EncodeShape<K, N, RPW, WV>;
   Plane16 acc[RPW];
   {
     const Plane16 x = lds_planes(set_planes + (K - 1) * 16);
@@ -243,19 +248,19 @@ __device__ __forceinline__ void encode_wave_group(const uint32_t *set_planes, co
 #pragma unroll
   for (int s = 0; s < RPW; ++s) {
     const int r = S::kPlan.rep[W][s];
-    if (r >= 0) store_replica(acc[s], a.outs[r] + out_off, sel);
+    if (r >= 0) store_replica(acc[s], a.outs[r] + out_off, bm);
   }
 }
 
-template <int K, int N, int RPW, int W>
+template <int K, int N, int RPW, int WV, int W>
 __device__ __forceinline__ void encode_dispatch(int wave, const uint32_t *set_planes, const FastEncodeArgs &a,
-                                                uint64_t out_off, uint32_t sel) {
-  using S = EncodeShape<K, N, RPW>;
+                                                uint64_t out_off, const BitMasks &bm) {
+  using S = EncodeShape<K, N, RPW, WV>;
   if constexpr (W < S::kWaves) {
     if (wave == W)
-      encode_wave_group<K, N, RPW, W>(set_planes, a, out_off, sel);
+      encode_wave_group<K, N, RPW, WV, W>(set_planes, a, out_off, bm);
     else
-      encode_dispatch<K, N, RPW, W + 1>(wave, set_planes, a, out_off, sel);
+      encode_dispatch<K, N, RPW, WV, W + 1>(wave, set_planes, a, out_off, bm);
   }
 }
 
@@ -292,14 +297,15 @@ __device__ __forceinline__ void stage_unpack(const typename StageVec<G>::type (&
   }
 }
 
-template <int K, int N, int RPW>
-__global__ __launch_bounds__((EncodeShape<K, N, RPW>::kThreads), 2) void k_encode_bs(FastEncodeArgs a) {
-  using S = EncodeShape<K, N, RPW>;
+template <int K, int N, int RPW, int WV>
+__global__ __launch_bounds__((EncodeShape<K, N, RPW, WV>::kThreads), (EncodeShape<K, N, RPW, WV>::kWavesPerSimd))
+void k_encode_bs(FastEncodeArgs a) {
+  using S = EncodeShape<K, N, RPW, WV>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t *my_set = lds + lane * S::kSetWords;
-  const uint32_t sel = (lane & 1) ? 0x03020706u : 0x05040100u;
+  const BitMasks bm = bit_masks();
 
   typename StageVec<S::kGroupsPerWave>::type P[32];
   uint32_t tile = blockIdx.x;
@@ -310,7 +316,7 @@ __global__ __launch_bounds__((EncodeShape<K, N, RPW>::kThreads), 2) void k_encod
     stage_unpack<S::kGroupsPerWave>(P, R);
 #pragma unroll
     for (int g = 0; g < S::kGroupsPerWave; ++g) {
-      transpose32(R[g]);
+      transpose32(R[g], bm);
       const int gw = wave * S::kGroupsPerWave + g;
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -328,9 +334,8 @@ __global__ __launch_bounds__((EncodeShape<K, N, RPW>::kThreads), 2) void k_encod
     // ---- evaluate this wave's replicas and store
     const uint32_t o = tile / a.tiles_per_obj;
     const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
-    const uint64_t out_off = (uint64_t)o * a.out_stride +
-                             2 * (stripe0 + ((lane & 1) ? (uint64_t)(lane - 1) + 1024 : (uint64_t)lane));
-    encode_dispatch<K, N, RPW, 0>(wave, my_set, a, out_off, sel);
+    const uint64_t out_off = (uint64_t)o * a.out_stride + 2 * (stripe0 + (uint64_t)lane);
+    encode_dispatch<K, N, RPW, WV, 0>(wave, my_set, a, out_off, bm);
     __syncthreads();
   }
 }
@@ -741,12 +746,12 @@ hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int K, int N, int RPW>
+template <int K, int N, int RPW, int WV>
 static hipError_t launch_encode_bs(const FastEncodeArgs &a, hipStream_t s) {
-  using S = EncodeShape<K, N, RPW>;
+  using S = EncodeShape<K, N, RPW, WV>;
   static bool configured = false;
   if (!configured) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_encode_bs<K, N, RPW>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_encode_bs<K, N, RPW, WV>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, S::kLdsBytes);
     if (e != hipSuccess) return e;
     configured = true;
@@ -755,18 +760,23 @@ static hipError_t launch_encode_bs(const FastEncodeArgs &a, hipStream_t s) {
   int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
   if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_encode_bs<K, N, RPW>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  hipLaunchKernelGGL((k_encode_bs<K, N, RPW, WV>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
   return hipGetLastError();
 }
+
+#ifndef VDS_ENC16_RPW  // replicas per wave / waves of the k=16, n=20 encode
+#define VDS_ENC16_RPW 5
+#define VDS_ENC16_WAVES 4
+#endif
 
 bool has_encode_fast(uint32_t k, uint32_t n) {
   return (k == 16 && n == 20) || (k == 32 && n == 40) || (k == 4 && n == 6);
 }
 
 hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, hipStream_t s) {
-  if (k == 16 && n == 20) return launch_encode_bs<16, 20, 5>(a, s);
-  if (k == 32 && n == 40) return launch_encode_bs<32, 40, 5>(a, s);
-  if (k == 4 && n == 6) return launch_encode_bs<4, 6, 3>(a, s);
+  if (k == 16 && n == 20) return launch_encode_bs<16, 20, VDS_ENC16_RPW, VDS_ENC16_WAVES>(a, s);
+  if (k == 32 && n == 40) return launch_encode_bs<32, 40, 5, 8>(a, s);
+  if (k == 4 && n == 6) return launch_encode_bs<4, 6, 3, 2>(a, s);
   return hipErrorNotSupported;
 }
 

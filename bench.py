@@ -103,6 +103,22 @@ def pmc_traffic(path, kernel, objects):
     return round(e["bytes_per_object"] * objects), f"{os.path.relpath(path, ROOT)}: {e['source']}"
 
 
+def owned_objects(rank: int, world: int, per_rank: int) -> list[int]:
+    """Global ids of the objects rank `rank` encodes and repairs: round-robin
+    ownership, object o -> rank o % world; every rank has
+    the same count, so per-GPU work is fixed as the world grows (weak scaling)."""
+    return [rank + world * i for i in range(per_rank)]
+
+
+def max_over_ranks(values, dist, device):
+    """Element-wise MAX of per-rank timings (the job finishes with its slowest
+    rank).  The only collective in the benchmark; none is on the data path."""
+    import torch
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,12 +156,14 @@ def main():
     per_obj = size + n * L + size
     if objects * per_obj > 0.92 * free:
         objects = max(1, int(0.92 * free // per_obj))
+    if world > 1:  # every rank runs the same count (weak scaling, value = world * objects)
+        objects = int(-max_over_ranks([-objects], dist, dev)[0])
     inp = torch.empty(objects * size, dtype=torch.uint8, device=dev)
     reps = torch.empty((n, objects * L), dtype=torch.uint8, device=dev)
     restored = torch.empty(objects * size, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    for i in range(objects):  # object o = rank + world * i (round-robin ownership)
-        chunk.fill_splitmix_device(inp[i * size:], size, SEED + rank + world * i)
+    for i, oid in enumerate(owned_objects(rank, world, objects)):
+        chunk.fill_splitmix_device(inp[i * size:], size, SEED + oid)
     torch.cuda.synchronize(dev)
 
     rep_ptrs = [reps[i].data_ptr() for i in range(n)]
@@ -186,9 +204,7 @@ def main():
     rep_ms = sum(b.elapsed_time(c) for _, b, c in ev) / args.steps
 
     if world > 1:
-        t = torch.tensor([elapsed, enc_ms, rep_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, enc_ms, rep_ms = (float(x) for x in t.tolist())
+        elapsed, enc_ms, rep_ms = max_over_ranks([elapsed, enc_ms, rep_ms], dist, dev)
 
     ms_per_step = elapsed / args.steps * 1e3
     total_bytes = world * objects * size

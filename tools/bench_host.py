@@ -1,0 +1,57 @@
+"""C5: host-resident objects, PCIe-inclusive rates.
+
+Encode: vds_ec_encode16_host_batch (pinned ring, H2D -> encode -> D2H of all n
+replicas, objects round-robin over the visible GPUs).  Repair:
+vds_ec_restore16_host per object (H2D of k replicas -> restore -> D2H).
+Prints one JSON line.  This rate is never bench.py's `value`.
+
+  python tools/bench_host.py [--objects 16] [--object-mib 64] [--k 16] [--m 4]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np  # noqa: E402
+
+from vds_amd import chunk  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--objects", type=int, default=16)
+p.add_argument("--object-mib", type=int, default=64)
+p.add_argument("--k", type=int, default=16)
+p.add_argument("--m", type=int, default=4)
+p.add_argument("--reps", type=int, default=2)
+a = p.parse_args()
+k, n, size = a.k, a.k + a.m, a.object_mib << 20
+rng = np.random.default_rng(1)
+objs = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(a.objects)]
+ids = list(range(n))
+L = chunk.replica_size(k, size)
+# caller-owned, pre-faulted replica buffers (a storage node writes into its own)
+outs = [[np.ones(L, dtype=np.uint8) for _ in ids] for _ in objs]
+chunk.encode_host_batch(k, ids, objs[:1], outs=outs[:1])  # warm-up: contexts, pinned rings
+best_enc = None
+for _ in range(a.reps):
+    t0 = time.perf_counter()
+    reps = chunk.encode_host_batch(k, ids, objs, outs=outs)
+    dt = time.perf_counter() - t0
+    best_enc = dt if best_enc is None else min(best_enc, dt)
+erased = list(range(0, n, max(1, n // a.m)))[: a.m]
+nodes = [r for r in range(n) if r not in erased][:k]
+store = chunk.ChunkStorage(k)
+best_rep = None
+for _ in range(a.reps):
+    t0 = time.perf_counter()
+    for o in range(a.objects):
+        out = store.restore_data({r: reps[o][r] for r in nodes})
+    dt = time.perf_counter() - t0
+    best_rep = dt if best_rep is None else min(best_rep, dt)
+assert out.tobytes() == objs[-1].tobytes()
+gib = a.objects * size / 2**30
+print(json.dumps({"metric": "host-resident (PCIe-inclusive) encode / repair GiB/s", "objects": a.objects,
+                  "object_bytes": size, "k": k, "n": n, "erased": erased,
+                  "encode_GiBps": round(gib / best_enc, 3), "repair_GiBps": round(gib / best_rep, 3),
+                  "encode_s": round(best_enc, 4), "repair_s": round(best_rep, 4)}), flush=True)

@@ -242,15 +242,19 @@ def fill_splitmix_device(dst, size: int, seed: int, stream=None) -> None:
     check(_lib.lib().vds_ec_fill_splitmix_device(ptr, size, seed, _stream_ptr(stream)), "fill_splitmix")
 
 
-def encode_host_batch(k: int, replicas: Sequence[int], objects: Sequence, max_devices: int = 0) -> list:
-    """Multi-GPU host-memory encode (one thread + pinned ring per device)."""
+def encode_host_batch(k: int, replicas: Sequence[int], objects: Sequence, max_devices: int = 0,
+                      outs: list | None = None) -> list:
+    """Multi-GPU host-memory encode (one thread + pinned ring per device).
+    `outs[o][i]` (optional) are caller-owned uint8 buffers of at least
+    replica_size(k, len(objects[o])) bytes that receive replica i of object o."""
     ids = _ids(replicas, 2)
     bufs = [_u8(o) for o in objects]
     sizes = np.array([b.size for b in bufs], dtype=np.uint64)
-    outs = []
-    for b in bufs:
-        L = replica_size(k, b.size)
-        outs.append([np.empty(max(L, 1), dtype=np.uint8) for _ in range(ids.size)])
+    if outs is None:
+        outs = [[np.empty(max(replica_size(k, b.size), 1), dtype=np.uint8) for _ in range(ids.size)] for b in bufs]
+    for row, b in zip(outs, bufs):
+        if len(row) != ids.size or any(_u8(o).size < replica_size(k, b.size) for o in row):
+            raise VdsEcError(_lib.EINVAL, "encode_host_batch: output buffer too small")
     optrs = (C.c_void_p * (len(bufs) * ids.size))(*[o.ctypes.data for row in outs for o in row])
     iptrs = (C.c_void_p * max(1, len(bufs)))(*[b.ctypes.data for b in bufs])
     check(_lib.lib().vds_ec_encode16_host_batch(k, _idp(ids, 2), ids.size, iptrs,

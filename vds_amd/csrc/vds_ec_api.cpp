@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -455,6 +456,80 @@ int check_restore_args(uint32_t k, const Id *nodes, const uint8_t *const *chunks
   return VDS_EC_OK;
 }
 
+// ------------------------------------------------- multi-GPU host batch
+// Pinned staging of the host batch path, one ring per device, created on
+// first use and kept (like HostCtx): hipHostMalloc of hundreds of MiB costs
+// more than the encode it feeds.
+struct BatchSlot {
+  hipStream_t stream = nullptr;
+  uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+  size_t in_cap = 0, out_cap = 0;
+  int64_t obj = -1;
+  int reserve(size_t in_b, size_t out_b) {
+    if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VDS_EC_ENODEV;
+    if (in_b > in_cap) {
+      if (h_in) (void)hipHostFree(h_in);
+      if (d_in) (void)hipFree(d_in);
+      h_in = d_in = nullptr;
+      in_cap = 0;
+      if (hipHostMalloc(&h_in, in_b, 0) != hipSuccess || hipMalloc(&d_in, in_b) != hipSuccess) return VDS_EC_ENOMEM;
+      in_cap = in_b;
+    }
+    if (out_b > out_cap) {
+      if (h_out) (void)hipHostFree(h_out);
+      if (d_out) (void)hipFree(d_out);
+      h_out = d_out = nullptr;
+      out_cap = 0;
+      if (hipHostMalloc(&h_out, out_b, 0) != hipSuccess || hipMalloc(&d_out, out_b) != hipSuccess)
+        return VDS_EC_ENOMEM;
+      out_cap = out_b;
+    }
+    return VDS_EC_OK;
+  }
+};
+
+struct BatchRing {
+  std::mutex mu;  // one batch call per device at a time
+  BatchSlot slot[2];
+};
+
+BatchRing *batch_ring(int dev) {
+  static std::mutex m;
+  static std::vector<BatchRing *> rings;
+  std::lock_guard<std::mutex> g(m);
+  if (dev < 0) return nullptr;
+  if ((size_t)dev >= rings.size()) rings.resize(dev + 1, nullptr);
+  if (!rings[dev]) rings[dev] = new BatchRing();  // never freed: outlives every caller
+  return rings[dev];
+}
+
+// Host copies of (dst, src) pairs of `bytes` each, split over a few threads:
+// one thread's memcpy into pinned memory runs far below host memory bandwidth.
+void parallel_copy(const std::vector<std::pair<uint8_t *, const uint8_t *>> &parts, size_t bytes) {
+  const size_t total = parts.size() * bytes;
+  const size_t kMinPerThread = 8u << 20;
+  size_t nt = total / kMinPerThread;
+  if (nt > 8) nt = 8;
+  if (nt <= 1) {
+    for (auto &p : parts) std::memcpy(p.first, p.second, bytes);
+    return;
+  }
+  // split the concatenation of all parts into nt equal ranges
+  auto run = [&](size_t t) {
+    size_t lo = total * t / nt, hi = total * (t + 1) / nt;
+    while (lo < hi) {
+      const size_t pi = lo / bytes, off = lo % bytes;
+      const size_t len = std::min(bytes - off, hi - lo);
+      std::memcpy(parts[pi].first + off, parts[pi].second + off, len);
+      lo += len;
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; ++t) th.emplace_back(run, t);
+  run(0);
+  for (auto &t : th) t.join();
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -668,66 +743,35 @@ int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
       status = VDS_EC_ENODEV;
       return;
     }
-    // Two slots per device: while one slot's object is on the GPU, the
-    // other's pinned staging is being filled / drained by this thread.
-    struct Slot {
-      hipStream_t stream = nullptr;
-      uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
-      size_t in_cap = 0, out_cap = 0;
-      int64_t obj = -1;
-    } slot[2];
-    auto release = [&]() {
-      for (auto &s : slot) {
-        if (s.stream) (void)hipStreamSynchronize(s.stream);
-        if (s.h_in) (void)hipHostFree(s.h_in);
-        if (s.h_out) (void)hipHostFree(s.h_out);
-        if (s.d_in) (void)hipFree(s.d_in);
-        if (s.d_out) (void)hipFree(s.d_out);
-        if (s.stream) (void)hipStreamDestroy(s.stream);
-      }
-    };
-    auto drain = [&](Slot &s) -> int {
+    // Two slots per device (persistent across calls): while one slot's
+    // object is on the GPU, the other's pinned staging is filled / drained.
+    BatchRing *ring = batch_ring(dev);
+    if (!ring) {
+      status = VDS_EC_ENODEV;
+      return;
+    }
+    std::lock_guard<std::mutex> hold(ring->mu);
+    auto drain = [&](BatchSlot &s) -> int {
       if (s.obj < 0) return VDS_EC_OK;
       hipError_t e = hipStreamSynchronize(s.stream);
       if (e != hipSuccess) return hip_status(e);
       const uint64_t L = vds_ec_replica_size(2, k, sizes[s.obj], flags);
-      for (uint32_t i = 0; i < n; ++i) std::memcpy(outs[(uint64_t)s.obj * n + i], s.h_out + i * L, L);
+      std::vector<std::pair<uint8_t *, const uint8_t *>> parts(n);
+      for (uint32_t i = 0; i < n; ++i) parts[i] = {outs[(uint64_t)s.obj * n + i], s.h_out + i * L};
+      parallel_copy(parts, L);
       s.obj = -1;
       return VDS_EC_OK;
     };
     int si = 0;
     for (int64_t o = dev; o < (int64_t)count && status.load() == VDS_EC_OK; o += ndev, si ^= 1) {
-      Slot &s = slot[si];
+      BatchSlot &s = ring->slot[si];
       int rc = drain(s);
       if (rc) { status = rc; break; }
       const uint64_t size = sizes[o];
       const uint64_t L = vds_ec_replica_size(2, k, size, flags);
-      const size_t in_b = size ? size : 1, out_b = L * n ? L * n : 1;
-      if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) {
-        status = VDS_EC_ENODEV;
-        break;
-      }
-      if (in_b > s.in_cap) {
-        if (s.h_in) (void)hipHostFree(s.h_in);
-        if (s.d_in) (void)hipFree(s.d_in);
-        s.h_in = s.d_in = nullptr;
-        if (hipHostMalloc(&s.h_in, in_b, 0) != hipSuccess || hipMalloc(&s.d_in, in_b) != hipSuccess) {
-          status = VDS_EC_ENOMEM;
-          break;
-        }
-        s.in_cap = in_b;
-      }
-      if (out_b > s.out_cap) {
-        if (s.h_out) (void)hipHostFree(s.h_out);
-        if (s.d_out) (void)hipFree(s.d_out);
-        s.h_out = s.d_out = nullptr;
-        if (hipHostMalloc(&s.h_out, out_b, 0) != hipSuccess || hipMalloc(&s.d_out, out_b) != hipSuccess) {
-          status = VDS_EC_ENOMEM;
-          break;
-        }
-        s.out_cap = out_b;
-      }
-      if (size) std::memcpy(s.h_in, objs[o], size);
+      rc = s.reserve(size ? size : 1, L * n ? L * n : 1);
+      if (rc) { status = rc; break; }
+      if (size) parallel_copy({{s.h_in, objs[o]}}, size);
       hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, size, hipMemcpyHostToDevice, s.stream);
       if (e != hipSuccess) { status = hip_status(e); break; }
       std::vector<uint8_t *> douts(n);
@@ -738,11 +782,11 @@ int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
       if (e != hipSuccess) { status = hip_status(e); break; }
       s.obj = o;
     }
-    for (auto &s : slot) {
+    for (auto &s : ring->slot) {
       int rc = drain(s);
       if (rc && status.load() == VDS_EC_OK) status = rc;
+      s.obj = -1;
     }
-    release();
   };
   std::vector<std::thread> threads;
   for (int d = 0; d < ndev; ++d) threads.emplace_back(worker, d);

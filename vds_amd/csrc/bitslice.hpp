@@ -12,6 +12,8 @@
 // reference (big-endian 16-bit cells, binary_serialize.cpp:18-22).
 #pragma once
 
+#include <utility>
+
 #include "gf_common.hpp"
 
 #if defined(__HIPCC__) || defined(__HIP__)
@@ -130,6 +132,72 @@ VDS_INLINE Plane16 plane_horner(const Plane16 &acc, const Plane16 &x) {
         return plane_xor(w, x);
     }
   }
+}
+
+// Multiplication by a constant C as a 16x16 bit matrix, stored as operand
+// lists: output plane i of (acc * C) is the XOR of acc planes j[i][0..n[i]),
+// i.e. of the planes j with bit i of C * x^j set.
+struct MulRowLists {
+  int8_t j[16][16];
+  int8_t n[16];
+};
+
+constexpr MulRowLists mul_row_lists(uint32_t C) {
+  MulRowLists L{};
+  for (int i = 0; i < 16; ++i) L.n[i] = 0;
+  for (int jj = 0; jj < 16; ++jj) {
+    const uint32_t v = gf16_mul(C, 1u << jj);
+    for (int i = 0; i < 16; ++i)
+      if ((v >> i) & 1u) L.j[i][L.n[i]++] = (int8_t)jj;
+  }
+  return L;
+}
+
+// VALU instructions of one row-form Horner step acc * C + x: every output
+// plane folds its n[i] acc planes and the x plane two at a time (xor3).
+constexpr int row_horner_cost(uint32_t C) {
+  if (C == 0) return 0;
+  const MulRowLists L = mul_row_lists(C);
+  int c = 0;
+  for (int i = 0; i < 16; ++i) c += (L.n[i] + 1) / 2;
+  return c;
+}
+
+template <uint32_t C>
+struct RowHorner {
+  static constexpr MulRowLists L = mul_row_lists(C);
+};
+
+template <uint32_t C, int I, int Q>
+VDS_INLINE uint32_t fold_row(uint32_t v, const Plane16 &acc) {
+  constexpr MulRowLists L = RowHorner<C>::L;
+  if constexpr (Q + 1 < L.n[I])
+    return fold_row<C, I, Q + 2>(xor3(v, acc.p[L.j[I][Q]], acc.p[L.j[I][Q + 1]]), acc);
+  else if constexpr (Q < L.n[I])
+    return v ^ acc.p[L.j[I][Q]];
+  else
+    return v;
+}
+
+template <uint32_t C, size_t... I>
+VDS_INLINE Plane16 row_horner_impl(const Plane16 &acc, const Plane16 &x, std::index_sequence<I...>) {
+  Plane16 out;
+  ((out.p[I] = fold_row<C, (int)I, 0>(x.p[I], acc)), ...);
+  return out;
+}
+
+// Horner step acc * C + x in row form: each output plane is one XOR of its
+// matrix row's acc planes and the x plane, folded into v_bitop3_b32 xor3s.
+// Unlike the x-shift chain (plane_horner) there is no plane renaming, so a
+// rolled loop needs no register copies, and the feedback XORs of the
+// reduction merge into the row sums (~27% fewer VALU ops
+// summed over replicas 0..19).
+template <uint32_t C>
+VDS_INLINE Plane16 plane_horner_rows(const Plane16 &acc, const Plane16 &x) {
+  if constexpr (C == 0)
+    return x;
+  else
+    return row_horner_impl<C>(acc, x, std::make_index_sequence<16>{});
 }
 
 // Multiply by a wave-uniform runtime constant c (< 2^16): Horner over all 16

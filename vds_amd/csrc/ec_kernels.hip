@@ -137,9 +137,10 @@ constexpr int popcount32(uint32_t v) {
   return c;
 }
 
-// Relative VALU cost of one Horner step for replica r (3 XOR per x-shift,
-// 16 per add): used to balance replicas across waves.
-constexpr int horner_cost(int r) { return r == 0 ? 1 : 3 * poly_degree((uint32_t)r) + 16 * popcount32((uint32_t)r); }
+
+// VALU cost of one row-form Horner step for replica r (bitslice.hpp): used
+// to balance replicas across waves.
+constexpr int horner_cost(int r) { return r == 0 ? 1 : row_horner_cost((uint32_t)r); }
 
 template <int N, int WAVES, int RPW>
 struct ReplicaPlan {
@@ -153,37 +154,48 @@ constexpr ReplicaPlan<N, WAVES, RPW> plan_replicas() {
   int load[WAVES] = {};
   int cnt[WAVES] = {};
   bool used[N] = {};
+  int cost[N] = {};
+  for (int r = 0; r < N; ++r) cost[r] = horner_cost(r);
   for (int w = 0; w < WAVES; ++w)
     for (int s = 0; s < RPW; ++s) p.rep[w][s] = -1;
   for (int it = 0; it < N; ++it) {
     int best = -1;
     for (int r = 0; r < N; ++r)
-      if (!used[r] && (best < 0 || horner_cost(r) > horner_cost(best))) best = r;
+      if (!used[r] && (best < 0 || cost[r] > cost[best])) best = r;
     used[best] = true;
     int bw = -1;
     for (int w = 0; w < WAVES; ++w)
       if (cnt[w] < RPW && (bw < 0 || load[w] < load[bw])) bw = w;
     p.rep[bw][cnt[bw]++] = best;
-    load[bw] += horner_cost(best);
+    load[bw] += cost[best];
   }
   return p;
 }
 
 template <int K, int N, int RPW, int WV>
 struct EncodeShape {
+  // Loads: every lane takes two dwords (4 cells) of each of its set's 32
+  // stripes, so K/4 lanes cover a stripe and one wave covers 256/K sets: a
+  // wave-load instruction reads 256/K whole consecutive stripes = 512 B
+  // contiguous.  The WV = K/4 waves then split the replicas.
   static constexpr int kWaves = WV;
   static constexpr int kThreads = kWaves * 64;
-  static constexpr int kWordGroups = K / 2;                 // dwords per stripe
-  static constexpr int kGroupsPerWave = kWordGroups / kWaves;
-  static constexpr int kSetWords = K * 16 + 4;              // planes per set + pad
-  static constexpr int kLdsBytes = 64 * kSetWords * 4;
-  // waves per SIMD the register budget is sized for: 2 (256 VGPRs) unless
-  // two 8-wave workgroups fit a CU (4, i.e. 128 VGPRs)
-  static constexpr int kWavesPerSimd = (WV >= 8 && 2 * kLdsBytes <= 160 * 1024) ? 4 : 2;
+  static constexpr int kLanesPerSet = K / 4;
+  static constexpr int kSetsPerWave = 64 / kLanesPerSet;
+  // LDS: set s (= the Horner lane) holds cell c's 16 planes at dword
+  // 16 c + kGroupPad (c / 4); the set stride is 4 mod 32 dwords.  Both the
+  // transposes' ds_write_b128 (lanes = cell groups of a few sets) and the
+  // Horner's ds_read_b128 (lanes = sets) are then bank-conflict free.
+  static constexpr int kGroupPad = (K % 32 == 0) ? 4 : 8;
+  static constexpr int kSetData = 16 * K + kGroupPad * (K / 4);
+  static constexpr int kSetWords = kSetData + ((4 - kSetData % 32) + 32) % 32;
+  static constexpr int kPlaneBytes = 64 * kSetWords * 4;
+  static constexpr int kLdsBytes = kPlaneBytes;
+  static constexpr int kWavesPerSimd = 2;  // 256 VGPRs: accumulators ping-pong + the prefetched tile
   static constexpr ReplicaPlan<N, kWaves, RPW> kPlan = plan_replicas<N, kWaves, RPW>();
-  static_assert(kWordGroups % kWaves == 0, "word groups must split evenly over waves");
+  static_assert(K % 4 == 0 && WV == K / 4, "fast encode: k % 4 == 0 and k/4 waves");
   static_assert(RPW * WV >= N, "every replica needs a wave");
-  static_assert(K % 2 == 0, "fast path needs even k");
+  __device__ __forceinline__ static constexpr int cell_off(int c) { return 16 * c + kGroupPad * (c >> 2); }
 };
 
 // Four ds_read_b128 per cell.  A volatile 128-bit load through an LDS
@@ -206,6 +218,10 @@ __device__ __forceinline__ Plane16 lds_planes(const uint32_t *p) {
   return x;
 }
 
+#ifndef VDS_DIAG_ENC  // diagnostic builds (timing only, wrong results): 1 = no stores and no output
+#define VDS_DIAG_ENC 0  // transposes, 2 = no Horner, 3 = no stores
+#endif
+
 // Transpose one replica's planes back to big-endian cells and store them.
 // After the transpose, word q of lane l holds the cells of stripes l + 64 q
 // (low half) and l + 1024 + 64 q (high half); each half goes out as a 2-byte
@@ -216,6 +232,9 @@ __device__ __forceinline__ void store_replica(const Plane16 &acc, uint8_t *base,
 #pragma unroll
   for (int j = 0; j < 16; ++j) rows[j] = acc.p[j ^ 8];  // word bit j <-> cell bit j^8 (BE)
   transpose16x2(rows, bm);
+#if VDS_DIAG_ENC == 3
+  if (((uintptr_t)base & 1) == 0) return;  // transposes kept, stores never run for real tiles
+#endif
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     *reinterpret_cast<uint16_t *>(base + 128 * q) = (uint16_t)rows[q];
@@ -223,78 +242,114 @@ __device__ __forceinline__ void store_replica(const Plane16 &acc, uint8_t *base,
   }
 }
 
-template <int K, int N, int RPW, int WV, int W>
-__device__ __forceinline__ void encode_wave_group(const uint32_t *set_planes, const FastEncodeArgs &a,
-                                                  uint64_t out_off, const BitMasks &bm) {
+// acc[s] <- acc[s] * r_s + x for this wave's replicas (replica 0 is skipped:
+// it is cell 0 itself and is taken from the last x).
+typedef __attribute__((address_space(3))) char lds_stage;
+
+// acc[i] <- acc[i] * r + x for replicas r = plan slots S0 .. S0+PR-1 of wave
+// W (replica 0, and empty slots, are skipped: replica 0 is cell 0 itself).
+template <int K, int N, int RPW, int WV, int W, int S0, int PR>
+__device__ __forceinline__ void rows_step(Plane16 (&dst)[PR], const Plane16 (&src)[PR], const Plane16 &x) {
   using S = EncodeShape<K, N, RPW, WV>;
-  Plane16 acc[RPW];
+  [&]<size_t... I>(std::index_sequence<I...>) {
+    constexpr auto rep = [](int i) { return S0 + i < RPW ? S::kPlan.rep[W][S0 + i] : -1; };
+    ((rep(I) > 0 ? (void)(dst[I] = plane_horner_rows<(uint32_t)(rep(I) > 0 ? rep(I) : 0)>(src[I], x)) : (void)0), ...);
+  }(std::make_index_sequence<PR>{});
+}
+
+// Store replica r's cells of this tile: `tile_off` is the tile's byte offset
+// in every replica, `lane_off` = 2 * lane the lane's own cell.
+
+__device__ __forceinline__ void store_rep(const Plane16 &acc, uint8_t *rep, uint64_t tile_off, lds_stage *, int lane,
+                                          const BitMasks &bm) {
+#if VDS_DIAG_ENC == 1
+  if (tile_off != 1) return;  // never stores for real tiles (offsets are even)
+#endif
+  store_replica(acc, rep + tile_off + 2 * lane, bm);
+}
+
+#ifndef VDS_ENC_PASS  // replicas evaluated per pass over the tile's cells
+#define VDS_ENC_PASS 3
+#endif
+
+// One pass: Horner for plan slots S0 .. S0+PR-1 over cells K-1 .. 0, then the
+// stores.  Two Horner steps per iteration, so the accumulators alternate
+// between A and B and the loop carries no register copies.  Splitting a
+// wave's replicas into passes spreads its stores over the tile instead of
+// one burst at the end (the kernel is write-bound when they bunch up).
+template <int K, int N, int RPW, int WV, int W, int S0, int PR>
+__device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const FastEncodeArgs &a, uint64_t tile_off,
+                                            lds_stage *stage, int lane, const BitMasks &bm) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  constexpr bool kAnyHorner = [] {
+    for (int s = S0; s < S0 + PR && s < RPW; ++s)
+      if (S::kPlan.rep[W][s] > 0) return true;
+    return false;
+  }();
+  if constexpr (!kAnyHorner) {  // only replica 0 (= cell 0) or empty slots
+#pragma unroll
+    for (int s = S0; s < S0 + PR && s < RPW; ++s)
+      if (S::kPlan.rep[W][s] == 0) store_rep(lds_planes(set_planes + S::cell_off(0)), a.outs[0], tile_off, stage, lane, bm);
+    return;
+  }
+  Plane16 A[PR], B[PR];
   {
-    const Plane16 x = lds_planes(set_planes + (K - 1) * 16);
+    const Plane16 x = lds_planes(set_planes + S::cell_off(K - 1));
 #pragma unroll
-    for (int s = 0; s < RPW; ++s) acc[s] = x;
+    for (int s = 0; s < PR; ++s) A[s] = x;
   }
-  Plane16 xn = lds_planes(set_planes + (K - 2) * 16);  // one cell ahead: LDS latency under the XORs
+  Plane16 xa = lds_planes(set_planes + S::cell_off(K - 2));
 #pragma clang loop unroll(disable)
-  for (int c = K - 2; c >= 0; --c) {
-    const Plane16 x = xn;
-    if (c > 0) xn = lds_planes(set_planes + (c - 1) * 16);
-    [&]<size_t... I>(std::index_sequence<I...>) {
-      ((S::kPlan.rep[W][I] >= 0
-            ? (void)(acc[I] = plane_horner<(uint32_t)(S::kPlan.rep[W][I] < 0 ? 0 : S::kPlan.rep[W][I])>(acc[I], x))
-            : (void)0),
-       ...);
-    }(std::make_index_sequence<RPW>{});
+  for (int c = K - 2; c >= 1 && VDS_DIAG_ENC != 2; c -= 2) {
+    const Plane16 xb = lds_planes(set_planes + S::cell_off(c - 1));
+    rows_step<K, N, RPW, WV, W, S0, PR>(B, A, xa);
+    xa = lds_planes(set_planes + S::cell_off(c - 2));
+    rows_step<K, N, RPW, WV, W, S0, PR>(A, B, xb);
   }
+  rows_step<K, N, RPW, WV, W, S0, PR>(A, A, xa);  // cell 0 (each step returns a fresh value)
 #pragma unroll
-  for (int s = 0; s < RPW; ++s) {
-    const int r = S::kPlan.rep[W][s];
-    if (r >= 0) store_replica(acc[s], a.outs[r] + out_off, bm);
+  for (int s = 0; s < PR; ++s) {
+    const int r = S0 + s < RPW ? S::kPlan.rep[W][S0 + s] : -1;
+    if (r == 0) store_rep(xa, a.outs[0], tile_off, stage, lane, bm);
+    if (r > 0) store_rep(A[s], a.outs[r], tile_off, stage, lane, bm);
+  }
+}
+
+template <int K, int N, int RPW, int WV, int W, int S0 = 0>
+__device__ __forceinline__ void encode_wave_group(const uint32_t *set_planes, const FastEncodeArgs &a,
+                                                  uint64_t tile_off, lds_stage *stage, int lane, const BitMasks &bm) {
+  constexpr int PR = VDS_ENC_PASS < RPW ? VDS_ENC_PASS : RPW;
+  if constexpr (S0 < RPW) {
+    encode_pass<K, N, RPW, WV, W, S0, PR>(set_planes, a, tile_off, stage, lane, bm);
+    encode_wave_group<K, N, RPW, WV, W, S0 + PR>(set_planes, a, tile_off, stage, lane, bm);
   }
 }
 
 template <int K, int N, int RPW, int WV, int W>
 __device__ __forceinline__ void encode_dispatch(int wave, const uint32_t *set_planes, const FastEncodeArgs &a,
-                                                uint64_t out_off, const BitMasks &bm) {
+                                                uint64_t tile_off, lds_stage *stage, int lane, const BitMasks &bm) {
   using S = EncodeShape<K, N, RPW, WV>;
   if constexpr (W < S::kWaves) {
     if (wave == W)
-      encode_wave_group<K, N, RPW, WV, W>(set_planes, a, out_off, bm);
+      encode_wave_group<K, N, RPW, WV, W>(set_planes, a, tile_off, stage, lane, bm);
     else
-      encode_dispatch<K, N, RPW, WV, W + 1>(wave, set_planes, a, out_off, bm);
+      encode_dispatch<K, N, RPW, WV, W + 1>(wave, set_planes, a, tile_off, stage, lane, bm);
   }
 }
 
-// Load this wave's word groups of the lane's 32 stripes of `tile`:
-// slot i of lane l <-> stripe stripe0 + l + 64 i.  The data stays in the
-// loaded vector registers (one uint32 x G vector per slot) until the next
-// iteration unpacks it, so no copy forces an early s_waitcnt.
-template <int G> struct StageVec;
-template <> struct StageVec<1> { typedef uint32_t type; };
-template <> struct StageVec<2> { typedef uint32_t type __attribute__((ext_vector_type(2))); };
-template <> struct StageVec<4> { typedef uint32_t type __attribute__((ext_vector_type(4))); };
+// Load dwords 2p, 2p+1 of the 32 stripes of set `set` of `tile`: slot i of a
+// set s <-> stripe stripe0 + s + 64 i.  The data stays in the loaded vector
+// registers until the next iteration unpacks it, so no copy forces an early
+// s_waitcnt.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-template <int K, int G>
-__device__ __forceinline__ void encode_load(typename StageVec<G>::type (&P)[32], const FastEncodeArgs &a,
-                                            uint32_t tile, int lane, int wave) {
+template <int K>
+__device__ __forceinline__ void encode_load(u32x2 (&P)[32], const FastEncodeArgs &a, uint32_t tile, int set, int p) {
   const uint32_t o = tile / a.tiles_per_obj;
   const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
-  const uint8_t *src = a.in + (uint64_t)o * a.in_stride + (stripe0 + lane) * (2 * K) + 4 * (wave * G);
+  const uint8_t *src = a.in + (uint64_t)o * a.in_stride + (stripe0 + set) * (2 * K) + 8 * p;
 #pragma unroll
-  for (int i = 0; i < 32; ++i)
-    P[i] = *reinterpret_cast<const typename StageVec<G>::type *>(src + (uint64_t)i * 64 * (2 * K));
-}
-
-template <int G>
-__device__ __forceinline__ void stage_unpack(const typename StageVec<G>::type (&P)[32], uint32_t (&R)[G][32]) {
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    if constexpr (G == 1) {
-      R[0][i] = P[i];
-    } else {
-#pragma unroll
-      for (int g = 0; g < G; ++g) R[g][i] = P[i][g];
-    }
-  }
+  for (int i = 0; i < 32; ++i) P[i] = *reinterpret_cast<const u32x2 *>(src + (uint64_t)i * 64 * (2 * K));
 }
 
 template <int K, int N, int RPW, int WV>
@@ -304,38 +359,46 @@ void k_encode_bs(FastEncodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint32_t *my_set = lds + lane * S::kSetWords;
+  // transposes: this lane's set and 4-cell group; Horner: lane = set
+  const int tset = wave * S::kSetsPerWave + lane / S::kLanesPerSet;
+  const int tp = lane % S::kLanesPerSet;
+  uint32_t *t_planes = lds + tset * S::kSetWords + S::cell_off(4 * tp);
+  const uint32_t *my_set = lds + lane * S::kSetWords;
+  lds_stage *stage = nullptr;  // (store staging through LDS measured slower: 2-byte stores are not the limit)
   const BitMasks bm = bit_masks();
 
-  typename StageVec<S::kGroupsPerWave>::type P[32];
+  u32x2 P[32];
   uint32_t tile = blockIdx.x;
-  if (tile < a.total_tiles) encode_load<K, S::kGroupsPerWave>(P, a, tile, lane, wave);
+  if (tile < a.total_tiles) encode_load<K>(P, a, tile, tset, tp);
   for (; tile < a.total_tiles; tile += gridDim.x) {
-    // ---- transpose to planes and publish in LDS: cell 2gw+h, bit b = R[g][16h + (b^8)]
-    uint32_t R[S::kGroupsPerWave][32];
-    stage_unpack<S::kGroupsPerWave>(P, R);
+    // ---- transpose to planes and publish in LDS: cell 4p+2g+h, bit b = R[g][16h + (b^8)]
+    uint32_t R[2][32];
 #pragma unroll
-    for (int g = 0; g < S::kGroupsPerWave; ++g) {
+    for (int i = 0; i < 32; ++i) {
+      R[0][i] = P[i].x;
+      R[1][i] = P[i].y;
+    }
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
       transpose32(R[g], bm);
-      const int gw = wave * S::kGroupsPerWave + g;
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int b0 = 16 * h + 4 * (m ^ 2);
-          *reinterpret_cast<uint4 *>(my_set + (2 * gw + h) * 16 + 4 * m) =
+          *reinterpret_cast<uint4 *>(t_planes + (2 * g + h) * 16 + 4 * m) =
               make_uint4(R[g][b0], R[g][b0 + 1], R[g][b0 + 2], R[g][b0 + 3]);
         }
     }
     __syncthreads();
     // ---- prefetch the next tile while this one is evaluated (software pipeline)
     const uint32_t next = tile + gridDim.x;
-    if (next < a.total_tiles) encode_load<K, S::kGroupsPerWave>(P, a, next, lane, wave);
+    if (next < a.total_tiles) encode_load<K>(P, a, next, tset, tp);
     // ---- evaluate this wave's replicas and store
     const uint32_t o = tile / a.tiles_per_obj;
     const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
-    const uint64_t out_off = (uint64_t)o * a.out_stride + 2 * (stripe0 + (uint64_t)lane);
-    encode_dispatch<K, N, RPW, WV, 0>(wave, my_set, a, out_off, bm);
+    const uint64_t tile_off = (uint64_t)o * a.out_stride + 2 * stripe0;
+    encode_dispatch<K, N, RPW, WV, 0>(wave, my_set, a, tile_off, stage, lane, bm);
     __syncthreads();
   }
 }
@@ -776,7 +839,7 @@ bool has_encode_fast(uint32_t k, uint32_t n) {
 hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, hipStream_t s) {
   if (k == 16 && n == 20) return launch_encode_bs<16, 20, VDS_ENC16_RPW, VDS_ENC16_WAVES>(a, s);
   if (k == 32 && n == 40) return launch_encode_bs<32, 40, 5, 8>(a, s);
-  if (k == 4 && n == 6) return launch_encode_bs<4, 6, 3, 2>(a, s);
+  if (k == 4 && n == 6) return launch_encode_bs<4, 6, 6, 1>(a, s);
   return hipErrorNotSupported;
 }
 

@@ -18,7 +18,7 @@
 // vds_amd/csrc/generated/restore_K_N.inc.  Points are processed in blocks so
 // the live temps of one block fit the register file.
 //
-//   gen_restore K N [syndrome_block interp_block] > restore_K_N.inc
+//   gen_restore K N WAVES syndrome_block interp_block [half_block] > restore_K_N_wW.inc
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -103,9 +103,17 @@ static Block make_block(const xorgen::XorProgram &p, int p0) {
   return B;
 }
 
+// Input point i of a program lives at LDS point i (par < 0) or 2 i + par
+// (the half-size interpolations read every other slot).
+static int g_par = -1;
+
 static void emit_loads(const Block &B, int bi) {
   for (int g = 0; g < B.n / 4; ++g)
-    if (B.group_used[g]) std::printf("    const auto g%d_%d = IN4(%d);\n", bi, g, 4 * B.p0 + g);
+    if (B.group_used[g]) {
+      const int pt = B.p0 + g / 4;
+      const int lds_pt = g_par < 0 ? pt : 2 * pt + g_par;
+      std::printf("    const auto g%d_%d = IN4(%d);\n", bi, g, 4 * lds_pt + g % 4);
+    }
 }
 
 // Emit a block's XORs; acc[] accumulates (first block: assigns).  Nodes are
@@ -204,12 +212,14 @@ static size_t emit_program(const char *name, const std::vector<std::vector<int>>
 }
 
 int main(int argc, char **argv) {
-  if (argc != 6) {
-    std::fprintf(stderr, "usage: %s K N WAVES syndrome_block interp_block\n", argv[0]);
+  if (argc != 6 && argc != 7) {
+    std::fprintf(stderr, "usage: %s K N WAVES syndrome_block interp_block [half_interp_block]\n", argv[0]);
     return 2;
   }
   const int K = std::atoi(argv[1]), N = std::atoi(argv[2]), M = N - K, waves = std::atoi(argv[3]);
   const int syn_pb = std::atoi(argv[4]), int_pb = std::atoi(argv[5]);
+  const int hb_pb = argc > 6 ? std::atoi(argv[6]) : 2;
+  size_t total_b = 0;
   if ((16 * M) % waves || (16 * K) % waves) {
     std::fprintf(stderr, "16 (N - K) and 16 K must split evenly over the waves\\n");
     return 2;
@@ -230,7 +240,7 @@ int main(int argc, char **argv) {
   std::vector<uint32_t> Vi(inv.begin(), inv.end());
   const int syn_rows = 16 * M / waves, int_rows = 16 * K / waves;
 
-  std::printf("// GENERATED by tools/xorgen/gen_restore %d %d %d %d %d -- do not edit.\n", K, N, waves, syn_pb, int_pb);
+  std::printf("// GENERATED by tools/xorgen/gen_restore %d %d %d %d %d %d -- do not edit.\n", K, N, waves, syn_pb, int_pb, hb_pb);
   std::printf("// Syndrome and fixed-interpolation XOR programs for k_restore_syn<%d,%d> with %d waves\n", K, N, waves);
   std::printf("// (points blocked by %d / %d; IN4(g) = planes 4g..4g+3, plane = 16 point + bit).\n", syn_pb, int_pb);
   std::printf("template <> struct RestorePrograms<%d, %d, %d> {\n", K, N, waves);
@@ -256,6 +266,29 @@ int main(int argc, char **argv) {
     std::snprintf(name, sizeof name, "interp%d", w);
     total += emit_program(name, vrows, K, int_rows * w, int_rows, int_pb);
   }
+  // Half-size interpolation for the one-level additive-FFT interpolation
+  // (k_restore_syn stage B): with G = {0, 2, .., K-2} and s(g) = g^2 + g,
+  // P(X) = P0(X^2+X) + X P1(X^2+X) where P0 / P1 (degree < K/2) take the
+  // values Q0 / Q1 at the K/2 points D = s(G), parked in LDS slots 2i / 2i+1.
+  // Wave w computes rows [16 K/4 (w % 2), +16 K/4) of P0 (w < 2) or P1.
+  const int H = K / 2, hb_rows = 16 * H / 2;
+  std::vector<uint16_t> dpts(H), dinv((size_t)H * H);
+  for (int i = 0; i < H; ++i) dpts[i] = (uint16_t)(gf16_mul(2 * i, 2 * i) ^ (2 * i));
+  if (vds_ec_inverse16(H, dpts.data(), dinv.data()) != VDS_EC_OK) return 1;
+  std::vector<uint32_t> Di(dinv.begin(), dinv.end());
+  const auto drows = all_bitrows(Di, H, H);
+  std::printf("  static constexpr int kHalfRows = %d;  // stage-B bit-rows per wave\n", hb_rows);
+  for (int w = 0; w < 4; ++w) {
+    char name[64];
+    std::snprintf(name, sizeof name, "interpB%d", w);
+    g_par = w / 2;
+    total_b += emit_program(name, drows, H, hb_rows * (w % 2), hb_rows, hb_pb);
+  }
+  g_par = -1;
+  std::printf("  template <typename In>\n  __device__ __forceinline__ static void interpB(int w, const In &IN4, uint32_t (&acc)[%d]) {\n", hb_rows);
+  std::printf("    switch (w) {\n");
+  for (int w = 0; w < 4; ++w) std::printf("      case %d: interpB%d(IN4, acc); break;\n", w, w);
+  std::printf("      default: break;\n    }\n  }\n");
   for (const char *kind : {"syndrome", "interp"}) {
     std::printf("  template <typename In>\n  __device__ __forceinline__ static void %s(int w, const In &IN4, uint32_t (&acc)[%d]) {\n",
                 kind, kind[0] == 's' ? syn_rows : int_rows);
@@ -264,7 +297,9 @@ int main(int argc, char **argv) {
     std::printf("      default: break;\n    }\n  }\n");
   }
   std::printf("  static constexpr int kXorOps = %zu;\n", total);
+  std::printf("  static constexpr int kXorOpsHalf = %zu;  // stage B (all four waves)\n", total_b);
   std::printf("};\n");
-  std::fprintf(stderr, "K=%d N=%d waves=%d: %zu XOR instructions per 32 stripes\n", K, N, waves, total);
+  std::fprintf(stderr, "K=%d N=%d waves=%d: %zu XOR instructions per 32 stripes (stage B: %zu)\n", K, N, waves, total,
+               total_b);
   return 0;
 }

@@ -547,6 +547,11 @@ struct SynShape {
 typedef __attribute__((address_space(3))) volatile u32x4 lds_v4;
 typedef __attribute__((address_space(3))) char lds_char;
 
+// Diagnostic builds (wrong results; timing only): VDS_DIAG_RES = 1 skips the
+// interpolation, 2 the stores, 3 the syndrome programs.
+#ifndef VDS_DIAG_RES
+#define VDS_DIAG_RES 0
+#endif
 // Diagnostic build switch (wrong results; timing only): every wave runs wave
 // 1's programs, to measure what the per-wave code footprint costs.
 #ifndef VDS_SYN_SAME_CODE
@@ -584,6 +589,92 @@ __device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t 
     v[4 * g + 1] = x[1];
     v[4 * g + 2] = x[2];
     v[4 * g + 3] = x[3];
+  }
+}
+
+#ifndef VDS_SYN_GM  // 1: interpolation by one additive-FFT level + half-size programs; 0: one 16-point program
+#define VDS_SYN_GM 1
+#endif
+
+// Interpolation from the fixed points F = {0..K-1} by one level of the
+// additive FFT (Gao-Mateer).  F is the GF(2)-span of 1, x, x^2, x^3, so with
+// G = {0, 2, .., K-2} (the span of x, x^2, x^3) and s(X) = X^2 + X (which maps
+// g and g+1 to the same point):
+//   P(X) = P0(s(X)) + X P1(s(X)),  deg P0, P1 < K/2,
+//   P1(s(g)) = c_g + c_{g+1},  P0(s(g)) = c_g + g P1(s(g)).
+// Stage A forms those K/2 value pairs in place (Q0 -> slot g, Q1 -> slot g+1),
+// stage B interpolates P0 and P1 on D = s(G) with generated XOR programs
+// (RestorePrograms::interpB), and stage C expands (X^2+X)^i = X^i (X+1)^i,
+// whose coefficients are binomials mod 2, so it is XORs only.  About 60% of
+// the XORs of the direct 16-point program (tools/xorgen/gen_restore.cpp).
+template <int W>
+__device__ __forceinline__ void syn_gm_stage_a(const SynLds &L) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    constexpr int kPairs[2] = {2 * W, 2 * W + 1};
+    const int i = kPairs[q];
+    Plane16 c0, c1;
+    syn_get_point(L, 2 * i, c0.p);
+    syn_get_point(L, 2 * i + 1, c1.p);
+    const Plane16 q1 = plane_xor(c0, c1);
+    Plane16 q0;
+    if (q == 0)
+      q0 = plane_horner_rows<(uint32_t)(4 * W)>(q1, c0);
+    else
+      q0 = plane_horner_rows<(uint32_t)(4 * W + 2)>(q1, c0);
+    syn_put_point(L, 2 * i, q0.p);
+    syn_put_point(L, 2 * i + 1, q1.p);
+  }
+}
+
+// Output cell k = sum over P0_i with C(i, k - i) odd and P1_i with
+// C(i, k - 1 - i) odd (Lucas: C(i, m) is odd iff m's bits are a subset of i's).
+// P0_i sits in LDS slot i, P1_i in slot 8 + i.
+template <int W>
+__device__ __forceinline__ void syn_gm_stage_c(const SynLds &L, uint32_t (&cells)[64]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int k = 4 * W + c;
+    uint32_t acc[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) acc[b] = 0u;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int i = t & 7;
+      const int m = t < 8 ? k - i : k - 1 - i;
+      if (m >= 0 && m <= i && (m & ~i) == 0) {
+        uint32_t v[16];
+        syn_get_point(L, t, v);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) acc[b] ^= v[b];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 16; ++b) cells[16 * c + b] = acc[b];
+  }
+}
+
+template <int K, int N, int WV, int W>
+__device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_t (&cells)[64]) {
+  static_assert(K == 16 && WV == 4, "the one-level interpolation is laid out for k = 16, 4 waves");
+  using P = RestorePrograms<K, N, WV>;
+  if constexpr (W < WV) {
+    if (wave != W) return syn_interp_gm<K, N, WV, W + 1>(wave, L, cells);
+    syn_gm_stage_a<W>(L);
+    __syncthreads();
+    uint32_t half[P::kHalfRows];
+    P::interpB(W, L, half);
+    __syncthreads();  // every wave has read its Q values
+    // P0 cells 4 (W % 2) .. (W < 2) or P1 cells (W >= 2) -> slots (W / 2) 8 + 4 (W % 2) + c
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint32_t v[16];
+#pragma unroll
+      for (int b = 0; b < 16; ++b) v[b] = half[16 * c + b];
+      syn_put_point(L, 8 * (W / 2) + 4 * (W % 2) + c, v);
+    }
+    __syncthreads();
+    syn_gm_stage_c<W>(L, cells);
   }
 }
 
@@ -655,7 +746,11 @@ void k_restore_syn(SynRestoreArgs a) {
     // ---- 2. syndrome bit-rows of this wave, parked in the erased slots
     {
       uint32_t syn[S::kSynRows];
+#if VDS_DIAG_RES == 3
+      for (int r = 0; r < S::kSynRows; ++r) syn[r] = lane + r;
+#else
       P::syndrome(kSynSameCode ? 1 : wave, L, syn);
+#endif
       if (tile + gridDim.x < a.total_tiles) load(tile + gridDim.x);
       __syncthreads();  // every wave is done reading the zeroed erased planes
 #pragma unroll
@@ -697,7 +792,13 @@ void k_restore_syn(SynRestoreArgs a) {
     // ---- 4. fixed interpolation from points 0..K-1, then big-endian stores
     {
       uint32_t cells[16 * S::kCells];
+#if VDS_DIAG_RES == 1
+      for (int r = 0; r < 16 * S::kCells; ++r) cells[r] = lane * r;
+#elif VDS_SYN_GM
+      syn_interp_gm<K, N, WV, 0>(wave, L, cells);
+#else
       P::interp(kSynSameCode ? 1 : wave, L, cells);
+#endif
       uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
       constexpr int kGroups = S::kCells / 2;  // word groups (2 cells) per wave
       if constexpr (kGroups == 2) {
@@ -735,6 +836,9 @@ void k_restore_syn(SynRestoreArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const u32x4 v = *(lds_v4 *)(r0 + 1056 * i);
+#if VDS_DIAG_RES == 2
+          if (a.out_stride == 1)
+#endif
           *reinterpret_cast<u32x4 *>(g0 + 1024 * i) = v;
         }
       } else {

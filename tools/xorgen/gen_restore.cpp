@@ -270,24 +270,24 @@ int main(int argc, char **argv) {
   // (k_restore_syn stage B): with G = {0, 2, .., K-2} and s(g) = g^2 + g,
   // P(X) = P0(X^2+X) + X P1(X^2+X) where P0 / P1 (degree < K/2) take the
   // values Q0 / Q1 at the K/2 points D = s(G), parked in LDS slots 2i / 2i+1.
-  // Wave w computes rows [16 K/4 (w % 2), +16 K/4) of P0 (w < 2) or P1.
-  const int H = K / 2, hb_rows = 16 * H / 2;
+  // Wave w computes rows [hb_rows (w % (waves/2)), +hb_rows) of P0 (w < waves/2) or P1.
+  const int H = K / 2, hb_parts = waves / 2, hb_rows = 16 * H / hb_parts;
   std::vector<uint16_t> dpts(H), dinv((size_t)H * H);
   for (int i = 0; i < H; ++i) dpts[i] = (uint16_t)(gf16_mul(2 * i, 2 * i) ^ (2 * i));
   if (vds_ec_inverse16(H, dpts.data(), dinv.data()) != VDS_EC_OK) return 1;
   std::vector<uint32_t> Di(dinv.begin(), dinv.end());
   const auto drows = all_bitrows(Di, H, H);
   std::printf("  static constexpr int kHalfRows = %d;  // stage-B bit-rows per wave\n", hb_rows);
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < waves; ++w) {
     char name[64];
     std::snprintf(name, sizeof name, "interpB%d", w);
-    g_par = w / 2;
-    total_b += emit_program(name, drows, H, hb_rows * (w % 2), hb_rows, hb_pb);
+    g_par = w / hb_parts;
+    total_b += emit_program(name, drows, H, hb_rows * (w % hb_parts), hb_rows, hb_pb);
   }
   g_par = -1;
   std::printf("  template <typename In>\n  __device__ __forceinline__ static void interpB(int w, const In &IN4, uint32_t (&acc)[%d]) {\n", hb_rows);
   std::printf("    switch (w) {\n");
-  for (int w = 0; w < 4; ++w) std::printf("      case %d: interpB%d(IN4, acc); break;\n", w, w);
+  for (int w = 0; w < waves; ++w) std::printf("      case %d: interpB%d(IN4, acc); break;\n", w, w);
   std::printf("      default: break;\n    }\n  }\n");
   for (const char *kind : {"syndrome", "interp"}) {
     std::printf("  template <typename In>\n  __device__ __forceinline__ static void %s(int w, const In &IN4, uint32_t (&acc)[%d]) {\n",

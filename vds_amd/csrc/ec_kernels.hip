@@ -517,11 +517,21 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
 // ============================================ erasure-pattern-independent restore
 
 template <int K, int N, int WV> struct RestorePrograms;
+// Waves per k_restore_syn<16,20> workgroup (two workgroups per CU either way).
+// 8 waves (128 VGPRs, 4 waves per SIMD) measured 984 against 1375 GiB/s for 4:
+// the doubled barrier fan-in and spills outweigh the occupancy.
+#ifndef VDS_SYN_WAVES
+#define VDS_SYN_WAVES 4
+#endif
 #define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #ifdef VDS_SYN_INC  // A/B builds of alternative generated programs
 #include VDS_SYN_INC
 #else
+#if VDS_SYN_WAVES == 8
+#include "generated/restore_16_20_w8.inc"
+#else
 #include "generated/restore_16_20_w4.inc"
+#endif
 #endif
 #undef VDS_SCHED_FENCE
 
@@ -607,41 +617,36 @@ __device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t 
 // (RestorePrograms::interpB), and stage C expands (X^2+X)^i = X^i (X+1)^i,
 // whose coefficients are binomials mod 2, so it is XORs only.  About 60% of
 // the XORs of the direct 16-point program (tools/xorgen/gen_restore.cpp).
-template <int W>
+template <int W, int NP, int Q = 0>
 __device__ __forceinline__ void syn_gm_stage_a(const SynLds &L) {
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    constexpr int kPairs[2] = {2 * W, 2 * W + 1};
-    const int i = kPairs[q];
+  if constexpr (Q < NP) {
+    constexpr int i = NP * W + Q;  // the pair (g, g + 1) = (2 i, 2 i + 1)
     Plane16 c0, c1;
     syn_get_point(L, 2 * i, c0.p);
     syn_get_point(L, 2 * i + 1, c1.p);
     const Plane16 q1 = plane_xor(c0, c1);
-    Plane16 q0;
-    if (q == 0)
-      q0 = plane_horner_rows<(uint32_t)(4 * W)>(q1, c0);
-    else
-      q0 = plane_horner_rows<(uint32_t)(4 * W + 2)>(q1, c0);
+    const Plane16 q0 = plane_horner_rows<(uint32_t)(2 * i)>(q1, c0);
     syn_put_point(L, 2 * i, q0.p);
     syn_put_point(L, 2 * i + 1, q1.p);
+    syn_gm_stage_a<W, NP, Q + 1>(L);
   }
 }
 
-// Output cell k = sum over P0_i with C(i, k - i) odd and P1_i with
-// C(i, k - 1 - i) odd (Lucas: C(i, m) is odd iff m's bits are a subset of i's).
-// P0_i sits in LDS slot i, P1_i in slot 8 + i.
-template <int W>
-__device__ __forceinline__ void syn_gm_stage_c(const SynLds &L, uint32_t (&cells)[64]) {
+// Output cell k = sum of P0_i with C(i, k - i) odd and of P1_i with
+// C(i, k - 1 - i) odd (Lucas: C(i, m) is odd iff the bits of m are a subset of
+// those of i).  P0_i sits in LDS slot i, P1_i in slot K/2 + i.
+template <int K, int W, int NC>
+__device__ __forceinline__ void syn_gm_stage_c(const SynLds &L, uint32_t (&cells)[16 * NC]) {
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int k = 4 * W + c;
+  for (int c = 0; c < NC; ++c) {
+    const int k = NC * W + c;
     uint32_t acc[16];
 #pragma unroll
     for (int b = 0; b < 16; ++b) acc[b] = 0u;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int i = t & 7;
-      const int m = t < 8 ? k - i : k - 1 - i;
+    for (int t = 0; t < K; ++t) {
+      const int i = t % (K / 2);
+      const int m = t < K / 2 ? k - i : k - 1 - i;
       if (m >= 0 && m <= i && (m & ~i) == 0) {
         uint32_t v[16];
         syn_get_point(L, t, v);
@@ -655,26 +660,29 @@ __device__ __forceinline__ void syn_gm_stage_c(const SynLds &L, uint32_t (&cells
 }
 
 template <int K, int N, int WV, int W>
-__device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_t (&cells)[64]) {
-  static_assert(K == 16 && WV == 4, "the one-level interpolation is laid out for k = 16, 4 waves");
+__device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)]) {
+  static_assert(K == 16 && (WV == 4 || WV == 8), "the one-level interpolation is laid out for k = 16");
   using P = RestorePrograms<K, N, WV>;
+  constexpr int kPairs = (K / 2) / WV;           // stage-A pairs per wave
+  constexpr int kHalfCells = P::kHalfRows / 16;  // stage-B cells per wave
+  constexpr int kParts = WV / 2;                 // waves per half-size polynomial
   if constexpr (W < WV) {
     if (wave != W) return syn_interp_gm<K, N, WV, W + 1>(wave, L, cells);
-    syn_gm_stage_a<W>(L);
+    syn_gm_stage_a<W, kPairs>(L);
     __syncthreads();
     uint32_t half[P::kHalfRows];
     P::interpB(W, L, half);
     __syncthreads();  // every wave has read its Q values
-    // P0 cells 4 (W % 2) .. (W < 2) or P1 cells (W >= 2) -> slots (W / 2) 8 + 4 (W % 2) + c
+    // P0 (W < kParts) or P1 cells kHalfCells (W % kParts) + c -> slot (K/2) (W / kParts) + ..
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < kHalfCells; ++c) {
       uint32_t v[16];
 #pragma unroll
       for (int b = 0; b < 16; ++b) v[b] = half[16 * c + b];
-      syn_put_point(L, 8 * (W / 2) + 4 * (W % 2) + c, v);
+      syn_put_point(L, (K / 2) * (W / kParts) + kHalfCells * (W % kParts) + c, v);
     }
     __syncthreads();
-    syn_gm_stage_c<W>(L, cells);
+    syn_gm_stage_c<K, W, K / WV>(L, cells);
   }
 }
 
@@ -801,15 +809,14 @@ void k_restore_syn(SynRestoreArgs a) {
 #endif
       uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
       constexpr int kGroups = S::kCells / 2;  // word groups (2 cells) per wave
-      if constexpr (kGroups == 2) {
+      if constexpr (K == 16) {
         // Stage the tile's output in LDS (the planes are dead once every wave
         // has interpolated), stripe-major with 16 bytes of padding after every
         // 16 stripes: the writes of one instruction then hit distinct banks,
         // and the copy-out is 16 contiguous bytes per lane, so every HBM
         // write is a whole 1 KiB wave-instruction (no partial lines).  One
         // word group at a time keeps 32, not 64, transposed rows live.
-        static_assert(K == 16 && WV == 4 && 2048 * 32 + 128 * 16 <= S::kLdsBytes,
-                      "staging layout is for 32-byte stripes, 4 waves");
+        static_assert(2048 * 32 + 128 * 16 <= S::kLdsBytes, "staging layout is for 32-byte stripes");
         __syncthreads();
 #pragma unroll
         for (int g = 0; g < kGroups; ++g) {
@@ -830,11 +837,13 @@ void k_restore_syn(SynRestoreArgs a) {
           }
         }
         __syncthreads();
-        // 16-byte chunk c = 64 (16 wave + i) + lane of the tile: stripe c/2, half c%2
-        const lds_char *r0 = L.base + 1056u * 16u * wave + 32u * (lane >> 1) + 16u * (lane >> 5) + 16u * (lane & 1);
-        uint8_t *g0 = dst + stripe0 * (2 * K) + 16384u * wave + 16u * lane;
+        // 16-byte chunk c = 64 (kChunks wave + i) + lane of the tile: stripe c/2, half c%2
+        constexpr int kChunks = 64 / WV;  // 1 KiB pieces of the tile each wave writes
+        const lds_char *r0 =
+            L.base + 1056u * kChunks * wave + 32u * (lane >> 1) + 16u * (lane >> 5) + 16u * (lane & 1);
+        uint8_t *g0 = dst + stripe0 * (2 * K) + 1024u * kChunks * wave + 16u * lane;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < kChunks; ++i) {
           const u32x4 v = *(lds_v4 *)(r0 + 1056 * i);
 #if VDS_DIAG_RES == 2
           if (a.out_stride == 1)
@@ -976,7 +985,7 @@ hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t
 
 bool has_restore_syn(uint32_t k, uint32_t n) { return k == 16 && n == 20; }
 
-constexpr int kSynWaves16 = 4;
+constexpr int kSynWaves16 = VDS_SYN_WAVES;
 
 const uint16_t *restore_syn_weights(uint32_t k, uint32_t n) {
   if (k == 16 && n == 20) return &RestorePrograms<16, 20, kSynWaves16>::kSyndromeW[0][0];

@@ -107,6 +107,19 @@ int vds_ec_restore8_device(uint8_t k, const uint8_t *nodes, const uint8_t *const
                            uint32_t count, uint8_t *out, uint64_t out_stride, unsigned flags,
                            void *stream);
 
+/* Regenerate lost replicas from k survivors without materialising the object
+ * (SURVEY.md 8(f) row 3).  The reference's repair restores the object and
+ * re-encodes it (sync_process.cpp:313-335 -> restore_async + save_data,
+ * dht_network_client.cpp:582-658); replica t is P(t) stripe by stripe, so one
+ * pass over the survivors yields it directly.  Survivor j (id nodes[j]) of
+ * object o at chunks[j] + o*chunk_stride (HOST array of k device pointers,
+ * chunk_size bytes = cells + BE16 trailer); replica targets[i] of object o is
+ * written to outs[i] + o*out_stride (chunk_size bytes, trailer included).
+ * Bytes equal chunk_generator(k, t).write(restore(...)) for valid replicas. */
+int vds_ec_regenerate16_device(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
+                               uint64_t chunk_stride, uint32_t count, const uint16_t *targets, uint32_t ntargets,
+                               uint8_t *const *outs, uint64_t out_stride, void *stream);
+
 /* ---------------------------------------------------------- host entry points
  * Same operations on host memory (pinned staging, H2D -> kernel -> D2H on
  * the calling thread's current device).  outs: n host buffers of
@@ -124,6 +137,11 @@ int vds_ec_restore16_host(uint16_t k, const uint16_t *nodes, const uint8_t *cons
                           uint64_t chunk_size, uint8_t *out, uint64_t *out_size, unsigned flags);
 int vds_ec_restore8_host(uint8_t k, const uint8_t *nodes, const uint8_t *const *chunks,
                          uint64_t chunk_size, uint8_t *out, uint64_t *out_size, unsigned flags);
+
+/* Host-memory form of vds_ec_regenerate16_device: chunks are k host buffers
+ * of chunk_size bytes, outs ntargets host buffers of chunk_size bytes.      */
+int vds_ec_regenerate16_host(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
+                             const uint16_t *targets, uint32_t ntargets, uint8_t *const *outs);
 
 /* Batched host-memory encode across every visible GPU (one host thread,
  * pinned ring and stream pair per device; object o -> device o % devices).
@@ -146,6 +164,10 @@ int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void
  * environment disables path 3 (for A/B measurements).                       */
 int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint64_t size);
 int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size);
+/* 3 = the regenerate rides the syndrome kernel (every target an erased point
+ * of a compiled (k, n)) for the full tiles, 1 = generic path only.          */
+int vds_ec_regenerate16_path(uint16_t k, const uint16_t *nodes, const uint16_t *targets, uint32_t ntargets,
+                             uint64_t chunk_size);
 
 #ifdef __cplusplus
 }

@@ -27,7 +27,8 @@ from ._lib import F_CELLS, F_NO_TRAILER, VdsEcError, check
 
 __all__ = [
     "ChunkGenerator", "ChunkRestore", "ChunkStorage", "chunk_cells", "replica_size",
-    "encode_device", "restore_device", "fill_splitmix_device", "encode_host_batch",
+    "encode_device", "restore_device", "fill_splitmix_device", "encode_host_batch", "regenerate_host",
+    "regenerate_device",
     "VdsEcError", "multipliers", "inverse",
 ]
 
@@ -197,6 +198,14 @@ class ChunkStorage:
         """Batched form of generate_replica for the save_temp / save_data loops."""
         return encode_host(self.min_horcrux, replicas, data)
 
+    def regenerate_replicas(self, horcruxes: Mapping[int, object], targets: Sequence[int]) -> list:
+        """Replicas `targets` from exactly min_horcrux equal-size horcruxes, in
+        one pass (the repair's restore_data + generate_replica, fused)."""
+        if self.min_horcrux != len(horcruxes):
+            raise VdsEcError(_lib.EINVAL, "Error at restoring data")
+        items = list(horcruxes.items())
+        return regenerate_host(self.min_horcrux, [r for r, _ in items], [v for _, v in items], targets)
+
     def restore_data(self, horcruxes: Mapping[int, object]) -> np.ndarray:
         if self.min_horcrux != len(horcruxes):
             raise VdsEcError(_lib.EINVAL, "Error at restoring data")  # chunk_storage.cpp:65-67
@@ -235,6 +244,32 @@ def restore_device(k: int, nodes: Sequence[int], chunks: Sequence[int], chunk_si
     out_ptr = out.data_ptr() if hasattr(out, "data_ptr") else int(out)
     check(_lib.lib().vds_ec_restore16_device(k, _idp(ids, 2), ptrs, chunk_size, chunk_stride, padding, count,
                                              out_ptr, out_stride, 0, _stream_ptr(stream)), "restore16_device")
+
+
+def regenerate_host(k: int, nodes: Sequence[int], chunks: Sequence, targets: Sequence[int]) -> list:
+    """vds_ec_regenerate16_host: replicas `targets` of one object from k
+    survivor replicas (host buffers), bytes as restore + re-encode."""
+    ids = _ids(nodes, 2)[:k]
+    tg = _ids(targets, 2)
+    bufs = [_u8(c) for c in chunks[:k]]
+    if len(bufs) < k or any(b.size != bufs[0].size for b in bufs):
+        raise VdsEcError(_lib.EINVAL, "regenerate")
+    size = bufs[0].size
+    outs = [np.empty(max(size, 1), dtype=np.uint8) for _ in range(tg.size)]
+    cp = (C.c_void_p * k)(*[b.ctypes.data for b in bufs])
+    op = (C.c_void_p * max(1, tg.size))(*[o.ctypes.data for o in outs])
+    check(_lib.lib().vds_ec_regenerate16_host(k, _idp(ids, 2), cp, size, _idp(tg, 2), tg.size, op), "regenerate")
+    return [o[:size] for o in outs]
+
+
+def regenerate_device(k: int, nodes: Sequence[int], chunks: Sequence[int], chunk_size: int, chunk_stride: int,
+                      count: int, targets: Sequence[int], outs: Sequence[int], out_stride: int, stream=None) -> None:
+    ids = _ids(nodes, 2)
+    tg = _ids(targets, 2)
+    cp = (C.c_void_p * ids.size)(*[int(c) for c in chunks])
+    op = (C.c_void_p * max(1, tg.size))(*[int(o) for o in outs])
+    check(_lib.lib().vds_ec_regenerate16_device(k, _idp(ids, 2), cp, chunk_size, chunk_stride, count, _idp(tg, 2),
+                                                tg.size, op, out_stride, _stream_ptr(stream)), "regenerate16_device")
 
 
 def fill_splitmix_device(dst, size: int, seed: int, stream=None) -> None:

@@ -94,13 +94,43 @@ struct SynRestoreArgs {
   // R = W_E^{-1} as bit selections: byte (b & 3) of solve_sel[i][b >> 2] has
   // bit j set iff bit b of R[i][j] is set (row i = erased[i], M <= 8)
   uint32_t solve_sel[kMaxFastK / 4][4];
+  // regenerate mode (k_restore_syn<..., true>): the recovered point erased[w]
+  // is written as replica bytes to regen[w] + o * regen_stride (nullptr: not
+  // requested); the interpolation is skipped
+  uint8_t *regen[kMaxFastK / 4];
+  uint64_t regen_stride;
+};
+
+constexpr int kInlineCoef = 512;  // regenerate coefficients carried in the kernel arguments
+
+// Generic regenerate (any k, any targets): replica targets[i] of object o is
+// sum_j coef[i][j] * chunk_j cell by cell (coef = V_targets V_S^{-1}, nt x k
+// row-major), for cells [t_begin, t_begin + t_count), then the trailer (cell
+// index T) copied from chunk 0 -- the bytes restore + re-encode would give
+// (sync_process.cpp:313-335 -> chunk.h:402-444 then chunk.h:245-281).
+struct RegenArgs {
+  const uint8_t *chunk_ptr[kInlineChunks];
+  const uint8_t *const *chunk_table;  // used when k > kInlineChunks
+  uint64_t chunk_stride;
+  const uint16_t *coef_dev;           // used when nt * k > kInlineCoef
+  uint32_t coef_inline[kInlineCoef / 2];
+  uint32_t count;
+  uint32_t k;
+  uint32_t cell_bytes;
+  uint32_t nt;
+  uint64_t t_begin;
+  uint64_t t_count;
+  uint64_t T;
+  uint8_t *outs[kMaxLaunchReplicas];
+  uint64_t out_stride;
 };
 
 hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s);
 bool has_restore_syn(uint32_t k, uint32_t n);
 // W[j][a] = v_a a^j of the syndrome map for (k, n); nullptr if not compiled.
 const uint16_t *restore_syn_weights(uint32_t k, uint32_t n);
-hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s);
+hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen = false);
+hipError_t launch_regen_generic(const RegenArgs &a, hipStream_t s);
 hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s);
 // Returns hipErrorNotSupported when no bit-sliced instantiation exists for (k, n).
 hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, hipStream_t s);

@@ -696,7 +696,7 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
 //     over the coefficient bits -- the only runtime-coefficient arithmetic;
 //  4. interpolates cells kCells*w.. from the fixed points 0..K-1 and stores
 //     them big-endian.
-template <int K, int N, int WV>
+template <int K, int N, int WV, bool REGEN>
 __global__ __launch_bounds__((SynShape<K, N, WV>::kThreads), (SynShape<K, N, WV>::kWavesPerSimd))
 void k_restore_syn(SynRestoreArgs a) {
   using S = SynShape<K, N, WV>;
@@ -797,6 +797,25 @@ void k_restore_syn(SynRestoreArgs a) {
       __syncthreads();
     }
     __syncthreads();
+    if constexpr (REGEN) {
+      // ---- 4'. regenerate: the recovered point e_w IS replica e_w's cells
+      // (P(e_w) stripe by stripe).  Undo the stage-1 transpose and store it as
+      // big-endian cells, one 1 KiB store per wave-instruction; no
+      // interpolation (fused "decode + re-encode" of sync_process.cpp:313-335).
+      if (wave < S::kM && a.regen[wave] != nullptr) {
+        uint32_t Pl[16], W[16];
+        syn_get_point(L, my_erased, Pl);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) W[b ^ 8] = Pl[b];
+        transpose16x2(W, bm);  // self-inverse: back to the loaded word layout
+        uint8_t *dst = a.regen[wave] + (uint64_t)o * a.regen_stride + 2 * stripe0 + 16 * lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<u32x4 *>(dst + 1024 * q) = u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]};
+      }
+      __syncthreads();  // every wave is done with this tile's planes
+      continue;
+    }
     // ---- 4. fixed interpolation from points 0..K-1, then big-endian stores
     {
       uint32_t cells[16 * S::kCells];
@@ -870,6 +889,46 @@ void k_restore_syn(SynRestoreArgs a) {
       }
     }
     __syncthreads();
+  }
+}
+
+// ========================================================= generic regenerate
+
+template <int CB>
+__global__ void k_regen_generic(RegenArgs a) {
+  const uint64_t per = a.t_count + 1;  // cells + the trailer
+  const uint64_t total = per * a.nt * (uint64_t)a.count;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t ti = idx % per;
+    const uint64_t rest = idx / per;
+    const uint32_t i = (uint32_t)(rest % a.nt);
+    const uint32_t o = (uint32_t)(rest / a.nt);
+    uint8_t *out = a.outs[i] + (uint64_t)o * a.out_stride;
+    auto chunk = [&](uint32_t j) {
+      return (a.chunk_table ? a.chunk_table[j] : a.chunk_ptr[j]) + (uint64_t)o * a.chunk_stride;
+    };
+    if (ti == a.t_count) {  // trailer BE16(size % (k*cell)), identical in every replica (chunk.h:273-275)
+      const uint8_t *c0 = chunk(0);
+      out[a.T * CB] = c0[a.T * CB];
+      out[a.T * CB + 1] = c0[a.T * CB + 1];
+      continue;
+    }
+    const uint64_t t = a.t_begin + ti;
+    uint32_t acc = 0;
+    for (uint32_t j = 0; j < a.k; ++j) {
+      const uint64_t e = (uint64_t)i * a.k + j;
+      const uint32_t coef = a.coef_dev ? a.coef_dev[e] : (a.coef_inline[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+      const uint8_t *c = chunk(j) + t * CB;
+      const uint32_t cell = CB == 2 ? (uint32_t)((c[0] << 8) | c[1]) : (uint32_t)c[0];
+      acc ^= gf_mul_cell<CB>(coef, cell);
+    }
+    if constexpr (CB == 2) {
+      out[2 * t] = (uint8_t)(acc >> 8);  // binary_serialize.cpp:18-22
+      out[2 * t + 1] = (uint8_t)(acc & 0xFF);
+    } else {
+      out[t] = (uint8_t)acc;
+    }
   }
 }
 
@@ -992,12 +1051,12 @@ const uint16_t *restore_syn_weights(uint32_t k, uint32_t n) {
   return nullptr;
 }
 
-template <int K, int N, int WV>
+template <int K, int N, int WV, bool REGEN>
 static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) {
   using S = SynShape<K, N, WV>;
   static bool configured = false;
   if (!configured) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_restore_syn<K, N, WV>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_restore_syn<K, N, WV, REGEN>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, S::kLdsBytes);
     if (e != hipSuccess) return e;
     configured = true;
@@ -1006,13 +1065,26 @@ static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) 
   int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
   if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_restore_syn<K, N, WV>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  hipLaunchKernelGGL((k_restore_syn<K, N, WV, REGEN>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s) {
-  if (k == 16 && n == 20) return launch_restore_syn_kn<16, 20, kSynWaves16>(a, s);
+hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen) {
+  if (k == 16 && n == 20)
+    return regen ? launch_restore_syn_kn<16, 20, kSynWaves16, true>(a, s)
+                 : launch_restore_syn_kn<16, 20, kSynWaves16, false>(a, s);
   return hipErrorNotSupported;
+}
+
+hipError_t launch_regen_generic(const RegenArgs &a, hipStream_t s) {
+  const uint64_t work = (a.t_count + 1) * a.nt * (uint64_t)a.count;
+  if (work == 0) return hipSuccess;
+  const int grid = grid_for(work, 256);
+  if (a.cell_bytes == 2)
+    hipLaunchKernelGGL(k_regen_generic<2>, dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_regen_generic<1>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed, hipStream_t s) {

@@ -448,6 +448,158 @@ int restore_host(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_t 
   return hip_status(hipStreamSynchronize(c.stream));
 }
 
+// ------------------------------------------------------ regenerate core
+// Replicas `targets` of objects restored from k survivors, without
+// materialising the object: replica t = P(t) stripe by stripe, with P the
+// polynomial through the survivors.  This is what sync_process's repair does
+// with restore_async + save_data (sync_process.cpp:313-335,
+// dht_network_client.cpp:582-658) -- decode, then re-encode -- fused.  For a
+// valid codeword the bytes are identical to that route; for survivors that
+// are not one codeword they are P(t) for the polynomial through the survivors
+// (the reference would trim and zero-pad the decoded object first).
+int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint8_t *const *chunks,
+                      uint64_t chunk_size, uint64_t chunk_stride, uint32_t count, const uint16_t *targets,
+                      uint32_t nt, uint8_t *const *outs, uint64_t out_stride, hipStream_t s) {
+  if (k == 0 || !nodes || !chunks || (nt > 0 && (!targets || !outs))) return VDS_EC_EINVAL;
+  if (chunk_size < 2 || (chunk_size - 2) % cb) return VDS_EC_EINVAL;  // cells + BE16 trailer
+  for (uint32_t j = 0; j < k; ++j)
+    if (!chunks[j]) return VDS_EC_EINVAL;
+  for (uint32_t i = 0; i < nt; ++i)
+    if (!outs[i]) return VDS_EC_EINVAL;
+  if (nt == 0 || count == 0) return VDS_EC_OK;
+  int rc = device_ready();
+  if (rc) return rc;
+  std::vector<uint16_t> inv((size_t)k * k);
+  if (cb == 2) {
+    rc = inverse16(k, nodes, inv.data());
+  } else {
+    std::vector<uint8_t> n8(nodes, nodes + k);
+    rc = inverse8(k, n8.data(), inv.data());
+  }
+  if (rc) return rc;
+  const uint64_t T = (chunk_size - 2) / cb;
+  uint64_t fast_stripes = 0;
+  SynRestoreArgs sa{};
+  uint32_t syn_n = 0;
+  if (cb == 2 && plan_restore_syn(k, nodes, sa, &syn_n)) {
+    // the fast kernel regenerates erased points only: every target must be one
+    bool all = true;
+    for (uint32_t i = 0; i < nt && all; ++i) {
+      bool hit = false;
+      for (uint32_t w = 0; w < syn_n - k; ++w)
+        if (sa.erased[w] == targets[i] && !sa.regen[w]) {  // (a repeated target: generic path)
+          sa.regen[w] = outs[i];
+          hit = true;
+        }
+      all = hit;
+    }
+    const uint64_t tiles = T / kTileStripes;
+    const uint64_t total = tiles * count;
+    if (all && tiles > 0 && total <= 0xFFFFFFFFull) {
+      for (uint32_t j = 0; j < k; ++j) sa.chunks[j] = chunks[j];
+      sa.chunk_stride = chunk_stride;
+      sa.regen_stride = out_stride;
+      sa.tiles_per_obj = (uint32_t)tiles;
+      sa.total_tiles = (uint32_t)total;
+      hipError_t e = launch_restore_syn(k, syn_n, sa, s, true);
+      if (e != hipSuccess) return hip_status(e);
+      fast_stripes = tiles * kTileStripes;
+    }
+  }
+  // generic path: the remaining cells and the trailers, <= 64 targets per launch
+  void *tmp_table = nullptr, *tmp_coef = nullptr;
+  hipError_t e = hipSuccess;
+  if (k > (uint32_t)kInlineChunks) {
+    e = hipMalloc(&tmp_table, sizeof(uint8_t *) * k);
+    if (e == hipSuccess) e = hipMemcpy(tmp_table, chunks, sizeof(uint8_t *) * k, hipMemcpyHostToDevice);
+  }
+  for (uint32_t base = 0; base < nt && e == hipSuccess; base += kMaxLaunchReplicas) {
+    RegenArgs ga{};
+    ga.nt = std::min<uint32_t>(nt - base, kMaxLaunchReplicas);
+    if (tmp_table)
+      ga.chunk_table = static_cast<const uint8_t *const *>(tmp_table);
+    else
+      for (uint32_t j = 0; j < k; ++j) ga.chunk_ptr[j] = chunks[j];
+    // coef[i][j] = sum_m t_i^m inv[m][j]  (P_m = sum_j inv[m][j] c_j)
+    std::vector<uint16_t> coef((size_t)ga.nt * k, 0);
+    for (uint32_t i = 0; i < ga.nt; ++i) {
+      const uint32_t t = targets[base + i];
+      for (uint32_t m = 0; m < k; ++m) {
+        const uint32_t tm = cb == 2 ? gf16_vandermonde(t, m) : (m == 0 ? 1u : gf8_pow(t, m));
+        if (!tm) continue;
+        for (uint32_t j = 0; j < k; ++j) {
+          const uint32_t v = inv[(size_t)m * k + j];
+          coef[(size_t)i * k + j] ^= (uint16_t)(cb == 2 ? gf16_mul(tm, v) : gf8_mul(tm, v));
+        }
+      }
+    }
+    if (coef.size() <= (size_t)kInlineCoef) {
+      for (size_t x = 0; x < coef.size(); ++x) ga.coef_inline[x >> 1] |= uint32_t(coef[x]) << (16 * (x & 1));
+    } else {
+      if (tmp_coef) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(tmp_coef);
+        tmp_coef = nullptr;
+      }
+      e = hipMalloc(&tmp_coef, sizeof(uint16_t) * coef.size());
+      if (e == hipSuccess) e = hipMemcpy(tmp_coef, coef.data(), sizeof(uint16_t) * coef.size(), hipMemcpyHostToDevice);
+      ga.coef_dev = static_cast<const uint16_t *>(tmp_coef);
+    }
+    if (e != hipSuccess) break;
+    ga.chunk_stride = chunk_stride;
+    ga.count = count;
+    ga.k = k;
+    ga.cell_bytes = cb;
+    ga.t_begin = fast_stripes;
+    ga.t_count = T - fast_stripes;
+    ga.T = T;
+    for (uint32_t i = 0; i < ga.nt; ++i) ga.outs[i] = outs[base + i];
+    ga.out_stride = out_stride;
+    e = launch_regen_generic(ga, s);
+  }
+  if (tmp_table || tmp_coef) {
+    const hipError_t se = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = se;
+    if (tmp_table) (void)hipFree(tmp_table);
+    if (tmp_coef) (void)hipFree(tmp_coef);
+  }
+  return hip_status(e);
+}
+
+int regenerate_host(unsigned cb, uint32_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
+                    const uint16_t *targets, uint32_t nt, uint8_t *const *outs) {
+  if (k == 0 || !nodes || !chunks || (nt > 0 && (!targets || !outs))) return VDS_EC_EINVAL;
+  if (chunk_size < 2 || (chunk_size - 2) % cb) return VDS_EC_EINVAL;
+  for (uint32_t j = 0; j < k; ++j)
+    if (!chunks[j]) return VDS_EC_EINVAL;
+  for (uint32_t i = 0; i < nt; ++i)
+    if (!outs[i]) return VDS_EC_EINVAL;
+  int rc = device_ready();
+  if (rc) return rc;
+  if (nt == 0) return VDS_EC_OK;
+  HostCtx *cp = host_ctx();
+  if (!cp) return VDS_EC_ENODEV;
+  HostCtx &c = *cp;
+  rc = c.ensure(chunk_size * k, chunk_size * nt);
+  if (rc) return rc;
+  std::vector<const uint8_t *> dchunks(k);
+  for (uint32_t j = 0; j < k; ++j) {
+    dchunks[j] = c.d_in + (uint64_t)j * chunk_size;
+    hipError_t e = hipMemcpyAsync(c.d_in + (uint64_t)j * chunk_size, chunks[j], chunk_size, hipMemcpyHostToDevice,
+                                  c.stream);
+    if (e != hipSuccess) return hip_status(e);
+  }
+  std::vector<uint8_t *> douts(nt);
+  for (uint32_t i = 0; i < nt; ++i) douts[i] = c.d_out + (uint64_t)i * chunk_size;
+  rc = regenerate_device(cb, k, nodes, dchunks.data(), chunk_size, 0, 1, targets, nt, douts.data(), 0, c.stream);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < nt; ++i) {
+    hipError_t e = hipMemcpyAsync(outs[i], douts[i], chunk_size, hipMemcpyDeviceToHost, c.stream);
+    if (e != hipSuccess) return hip_status(e);
+  }
+  return hip_status(hipStreamSynchronize(c.stream));
+}
+
 template <typename Id>
 int check_restore_args(uint32_t k, const Id *nodes, const uint8_t *const *chunks, uint64_t chunk_size) {
   if (k == 0 || !nodes || !chunks) return VDS_EC_EINVAL;
@@ -792,6 +944,32 @@ int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
   for (int d = 0; d < ndev; ++d) threads.emplace_back(worker, d);
   for (auto &t : threads) t.join();
   return status.load();
+}
+
+int vds_ec_regenerate16_device(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
+                               uint64_t chunk_stride, uint32_t count, const uint16_t *targets, uint32_t ntargets,
+                               uint8_t *const *outs, uint64_t out_stride, void *stream) {
+  return regenerate_device(2, k, nodes, chunks, chunk_size, chunk_stride, count, targets, ntargets, outs, out_stride,
+                           as_stream(stream));
+}
+
+int vds_ec_regenerate16_host(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
+                             const uint16_t *targets, uint32_t ntargets, uint8_t *const *outs) {
+  return regenerate_host(2, k, nodes, chunks, chunk_size, targets, ntargets, outs);
+}
+
+int vds_ec_regenerate16_path(uint16_t k, const uint16_t *nodes, const uint16_t *targets, uint32_t ntargets,
+                             uint64_t chunk_size) {
+  if (k == 0 || !nodes || (ntargets && !targets) || chunk_size < 2) return 0;
+  SynRestoreArgs sa{};
+  uint32_t n = 0;
+  if ((chunk_size - 2) / 2 < kTileStripes || !plan_restore_syn(k, nodes, sa, &n)) return 1;
+  for (uint32_t i = 0; i < ntargets; ++i) {
+    bool hit = false;
+    for (uint32_t w = 0; w < n - k; ++w) hit |= sa.erased[w] == targets[i];
+    if (!hit) return 1;
+  }
+  return 3;
 }
 
 int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void *stream) {

@@ -228,6 +228,20 @@ def main():
     if world > 1:
         elapsed, enc_ms, rep_ms = max_over_ranks([elapsed, enc_ms, rep_ms], dist, dev)
 
+    # Replica names, also beside the metric: SHA-256 of
+    # every replica of the batch, one lane per replica (reps is [n][objects][L]).
+    digests = torch.empty((n * objects, 32), dtype=torch.uint8, device=dev)
+    chunk.sha256_device(reps, L, L, n * objects, digests)
+    torch.cuda.synchronize(dev)
+    h0, h1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    h0.record(stream)
+    chunk.sha256_device(reps, L, L, n * objects, digests)
+    h1.record(stream)
+    torch.cuda.synchronize(dev)
+    sha_ms = h0.elapsed_time(h1)
+    if world > 1:
+        sha_ms = max_over_ranks([sha_ms], dist, dev)[0]
+
     ms_per_step = elapsed / args.steps * 1e3
     total_bytes = world * objects * size
     value = total_bytes / (elapsed / args.steps) / 2**30
@@ -265,6 +279,7 @@ def main():
         "repair_ms": round(rep_ms, 3),
         "regenerate_GiBps": round(world * objects * size / (regen_ms * 1e-3) / 2**30, 3) if regen_ms else None,
         "regenerate_ms": round(regen_ms, 3) if regen_ms else None,
+        "sha256_replicas_GiBps": round(world * objects * n * L / (sha_ms * 1e-3) / 2**30, 3),
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "traffic_source": traffic_src, "algorithmic_bytes_per_launch": dom_bytes,

@@ -151,6 +151,19 @@ int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
                                const uint8_t *const *objs, const uint64_t *sizes, uint32_t count,
                                uint8_t *const *outs, unsigned flags, int max_devices);
 
+/* ---------------------------------------------------------- replica names
+ * The reference names each replica by SHA-256 of its bytes (save_temp /
+ * save_data: dht_network_client.cpp:79, :593 -> hash::signature(sha256),
+ * kernel/vds_crypto/hash.cpp:91-101, OpenSSL EVP_sha256).  Digests of count
+ * device messages of len bytes at base + j*stride (any alignment) go to
+ * digests + 32*j (device memory).                                             */
+int vds_ec_sha256_device(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count, uint8_t *digests,
+                         void *stream);
+/* vds_ec_encode16_host plus the SHA-256 of every replica, computed on the
+ * device before the copy-back: digests receives n*32 bytes (host).          */
+int vds_ec_encode16_hash_host(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data, uint64_t size,
+                              uint8_t *const *outs, uint8_t *digests, unsigned flags);
+
 /* ----------------------------------------------------------------- utilities */
 /* Fill `size` device bytes at dst with the splitmix64 stream of `seed`
  * (little-endian 8-byte words) -- the synthetic-object generator used by

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvds_ec.so")
-SOURCES = ["ec_kernels.hip", "vds_ec_api.cpp"]
+SOURCES = ["ec_kernels.hip", "sha256.hip", "vds_ec_api.cpp"]
 HEADERS = ["bitslice.hpp", "gf_common.hpp", "ec_internal.hpp"]
 ARCH = os.environ.get("VDS_EC_ARCH", "gfx950")
 

@@ -28,7 +28,7 @@ from ._lib import F_CELLS, F_NO_TRAILER, VdsEcError, check
 __all__ = [
     "ChunkGenerator", "ChunkRestore", "ChunkStorage", "chunk_cells", "replica_size",
     "encode_device", "restore_device", "fill_splitmix_device", "encode_host_batch", "regenerate_host",
-    "regenerate_device",
+    "regenerate_device", "sha256_device", "encode_hash_host",
     "VdsEcError", "multipliers", "inverse",
 ]
 
@@ -270,6 +270,30 @@ def regenerate_device(k: int, nodes: Sequence[int], chunks: Sequence[int], chunk
     op = (C.c_void_p * max(1, tg.size))(*[int(o) for o in outs])
     check(_lib.lib().vds_ec_regenerate16_device(k, _idp(ids, 2), cp, chunk_size, chunk_stride, count, _idp(tg, 2),
                                                 tg.size, op, out_stride, _stream_ptr(stream)), "regenerate16_device")
+
+
+def sha256_device(base, length: int, stride: int, count: int, digests, stream=None) -> None:
+    """SHA-256 of `count` device messages of `length` bytes at base + j*stride
+    into digests (device, 32*count bytes): the replica names of
+    dht_network_client.cpp:79 / :593."""
+    bp = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
+    dp = digests.data_ptr() if hasattr(digests, "data_ptr") else int(digests)
+    check(_lib.lib().vds_ec_sha256_device(bp, length, stride, count, dp, _stream_ptr(stream)), "sha256_device")
+
+
+def encode_hash_host(k: int, replicas: Sequence[int], data, write_padding: bool = True):
+    """All requested replicas of one host object plus their SHA-256 names
+    (save_temp / save_data: write, then hash::signature(sha256, replica))."""
+    buf = _u8(data)
+    ids = _ids(replicas, 2)
+    flags = 0 if write_padding else F_NO_TRAILER
+    L = replica_size(k, buf.size, 2, write_padding)
+    outs = [np.empty(max(L, 1), dtype=np.uint8) for _ in range(ids.size)]
+    digests = np.empty((max(1, ids.size), 32), dtype=np.uint8)
+    ptrs = (C.c_void_p * max(1, ids.size))(*[o.ctypes.data for o in outs])
+    check(_lib.lib().vds_ec_encode16_hash_host(k, _idp(ids, 2), ids.size, buf.ctypes.data if buf.size else None,
+                                               buf.size, ptrs, digests.ctypes.data, flags), "encode16_hash_host")
+    return [o[:L] for o in outs], [bytes(d) for d in digests[: ids.size]]
 
 
 def fill_splitmix_device(dst, size: int, seed: int, stream=None) -> None:

@@ -137,6 +137,9 @@ hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, h
 bool has_encode_fast(uint32_t k, uint32_t n);
 hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t s);
 bool has_restore_fast(uint32_t k);
+// SHA-256 of count messages of len bytes at base + j * stride -> digests + 32 j (sha256.hip).
+hipError_t launch_sha256(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count, uint8_t *digests,
+                         hipStream_t s);
 hipError_t launch_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed, hipStream_t s);
 
 }  // namespace vds_ec

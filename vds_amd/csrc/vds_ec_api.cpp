@@ -946,6 +946,47 @@ int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
   return status.load();
 }
 
+int vds_ec_sha256_device(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count, uint8_t *digests,
+                         void *stream) {
+  if (count && (!digests || (len && !base))) return VDS_EC_EINVAL;
+  if (count == 0) return VDS_EC_OK;
+  int rc = device_ready();
+  if (rc) return rc;
+  return hip_status(launch_sha256(base, len, stride, count, digests, as_stream(stream)));
+}
+
+int vds_ec_encode16_hash_host(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data, uint64_t size,
+                              uint8_t *const *outs, uint8_t *digests, unsigned flags) {
+  if (k == 0 || (n > 0 && (!replicas || !outs || !digests)) || (size > 0 && !data)) return VDS_EC_EINVAL;
+  int rc = device_ready();
+  if (rc) return rc;
+  if (n == 0) return VDS_EC_OK;
+  const uint64_t L = vds_ec_replica_size(2, k, size, flags);
+  HostCtx *cp = host_ctx();
+  if (!cp) return VDS_EC_ENODEV;
+  HostCtx &c = *cp;
+  rc = c.ensure(size ? size : 1, L * n ? L * n : 1);
+  if (!rc) rc = c.grow(&c.d_param, &c.d_param_cap, 32ull * n);
+  if (rc) return rc;
+  hipError_t e = hipSuccess;
+  if (size) e = hipMemcpyAsync(c.d_in, data, size, hipMemcpyHostToDevice, c.stream);
+  if (e != hipSuccess) return hip_status(e);
+  std::vector<uint8_t *> douts(n);
+  for (uint32_t i = 0; i < n; ++i) douts[i] = c.d_out + (uint64_t)i * L;
+  rc = encode_device(2, k, replicas, n, c.d_in, size, size, 1, douts.data(), 0, flags, c.stream);
+  if (rc) return rc;
+  // the replica hashes of save_temp / save_data (dht_network_client.cpp:79, :593), on the device
+  e = launch_sha256(c.d_out, L, L, n, c.d_param, c.stream);
+  if (e != hipSuccess) return hip_status(e);
+  for (uint32_t i = 0; i < n && L; ++i) {
+    e = hipMemcpyAsync(outs[i], douts[i], L, hipMemcpyDeviceToHost, c.stream);
+    if (e != hipSuccess) return hip_status(e);
+  }
+  e = hipMemcpyAsync(digests, c.d_param, 32ull * n, hipMemcpyDeviceToHost, c.stream);
+  if (e != hipSuccess) return hip_status(e);
+  return hip_status(hipStreamSynchronize(c.stream));
+}
+
 int vds_ec_regenerate16_device(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
                                uint64_t chunk_stride, uint32_t count, const uint16_t *targets, uint32_t ntargets,
                                uint8_t *const *outs, uint64_t out_stride, void *stream) {

@@ -114,6 +114,40 @@ static void chunk_test_storage() {
   ASSERT_EQ(0, std::memcmp(data.data(), result.data(), size));
 }
 
+// The repair route of sync_process.cpp:313-335 (restore_data, then
+// generate_replica of the missing replicas) against the fused
+// regenerate_replicas, and the batched replica names against the replicas.
+static void chunk_test_regenerate() {
+  const uint16_t k = 16, n = 20;
+  const int size = 3 * 65536 + std::rand() % 5000;
+  std::vector<uint8_t> data(size);
+  for (auto &d : data) d = uint8_t(std::rand());
+  vds::chunk_storage storage(k);
+  std::vector<uint16_t> ids(n);
+  for (uint16_t i = 0; i < n; ++i) ids[i] = i;
+  std::vector<vds::const_data_buffer> names;
+  GET_EXPECTED_TEST(reps, storage.generate_replicas(ids, data.data(), size, names));
+  ASSERT_EQ(size_t(n), reps.size());
+  ASSERT_EQ(size_t(n), names.size());
+  std::unordered_map<uint16_t, vds::const_data_buffer> survivors;
+  for (uint16_t r = 0; r < n; ++r)
+    if (r % 5) survivors[r] = reps[r];
+  GET_EXPECTED_TEST(object, storage.restore_data(survivors));
+  const std::vector<uint16_t> lost = {0, 5, 10, 15};
+  GET_EXPECTED_TEST(fused, storage.regenerate_replicas(survivors, lost));
+  for (size_t i = 0; i < lost.size(); ++i) {
+    GET_EXPECTED_TEST(again, storage.generate_replica(lost[i], object.data(), object.size()));
+    ASSERT_EQ(again.size(), fused[i].size());
+    ASSERT_EQ(0, std::memcmp(again.data(), fused[i].data(), again.size()));
+    ASSERT_EQ(0, std::memcmp(reps[lost[i]].data(), fused[i].data(), again.size()));
+  }
+  // names: the replica hash is a function of the bytes only
+  for (uint16_t r = 0; r < n; ++r) {
+    ASSERT_EQ(size_t(32), names[r].size());
+    for (uint16_t q = 0; q < r; ++q) ASSERT_EQ(false, std::memcmp(names[r].data(), names[q].data(), 32) == 0);
+  }
+}
+
 // chunk_output_async (chunk.h:116-176) is byte-identical to one-shot write.
 struct collect : vds::stream_output_async<uint8_t> {
   std::vector<uint8_t> bytes;
@@ -160,6 +194,7 @@ int main(int argc, char **argv) {
     for (int i = 0; i < 20; ++i) chunk_roundtrip<uint8_t>(0xFF);
     for (int i = 0; i < 20; ++i) chunk_roundtrip<uint16_t>(0xFFFF);
     chunk_test_storage();
+    chunk_test_regenerate();
     chunk_test_output_async();
   }
   std::printf("%s %s (%d failures)\n", mode.c_str(), g_fail ? "FAILED" : "OK", g_fail);

@@ -38,6 +38,47 @@ class _chunk_storage {
     return result;
   }
 
+  expected<std::vector<const_data_buffer>> generate_replicas(const std::vector<uint16_t> &replicas, const void *data,
+                                                             size_t size, std::vector<const_data_buffer> &hashes) {
+    const uint64_t len = vds_ec_replica_size(2, min_horcrux_, size, 0);
+    std::vector<std::vector<uint8_t>> bufs(replicas.size(), std::vector<uint8_t>(len ? len : 1));
+    std::vector<uint8_t *> outs(replicas.size());
+    for (size_t i = 0; i < replicas.size(); ++i) outs[i] = bufs[i].data();
+    std::vector<uint8_t> names(32 * (replicas.size() ? replicas.size() : 1));
+    const int rc = vds_ec_encode16_hash_host(min_horcrux_, replicas.data(), uint32_t(replicas.size()),
+                                             static_cast<const uint8_t *>(data), size, outs.data(), names.data(), 0);
+    if (rc != VDS_EC_OK) return make_unexpected<std::runtime_error>(vds_ec_strerror(rc));
+    std::vector<const_data_buffer> result;
+    hashes.clear();
+    for (size_t i = 0; i < bufs.size(); ++i) {
+      result.emplace_back(bufs[i].data(), len);
+      hashes.emplace_back(names.data() + 32 * i, 32);
+    }
+    return result;
+  }
+
+  expected<std::vector<const_data_buffer>> regenerate_replicas(
+      const std::unordered_map<uint16_t, const_data_buffer> &horcruxes, const std::vector<uint16_t> &targets) {
+    if (min_horcrux_ != horcruxes.size()) return make_unexpected<std::runtime_error>("Error at restoring data");
+    const size_t size = horcruxes.begin()->second.size();
+    std::vector<uint16_t> nodes;
+    std::vector<const uint8_t *> chunks;
+    for (auto &p : horcruxes) {
+      if (size != p.second.size()) return make_unexpected<std::runtime_error>("Error at restoring data");
+      nodes.push_back(p.first);
+      chunks.push_back(p.second.data());
+    }
+    std::vector<std::vector<uint8_t>> bufs(targets.size(), std::vector<uint8_t>(size ? size : 1));
+    std::vector<uint8_t *> outs(targets.size());
+    for (size_t i = 0; i < targets.size(); ++i) outs[i] = bufs[i].data();
+    const int rc = vds_ec_regenerate16_host(min_horcrux_, nodes.data(), chunks.data(), size, targets.data(),
+                                            uint32_t(targets.size()), outs.data());
+    if (rc != VDS_EC_OK) return make_unexpected<std::runtime_error>(vds_ec_strerror(rc));
+    std::vector<const_data_buffer> result;
+    for (auto &b : bufs) result.emplace_back(b.data(), size);
+    return result;
+  }
+
   // chunk_storage.cpp:62-86: exactly k equal-size horcruxes.
   expected<const_data_buffer> restore_data(const std::unordered_map<uint16_t, const_data_buffer> &horcruxes) {
     if (min_horcrux_ != horcruxes.size()) return make_unexpected<std::runtime_error>("Error at restoring data");
@@ -68,6 +109,17 @@ expected<const_data_buffer> chunk_storage::generate_replica(uint16_t replica, co
 expected<std::vector<const_data_buffer>> chunk_storage::generate_replicas(const std::vector<uint16_t> &replicas,
                                                                           const void *data, size_t size) {
   return impl_->generate_replicas(replicas, data, size);
+}
+
+expected<std::vector<const_data_buffer>> chunk_storage::generate_replicas(const std::vector<uint16_t> &replicas,
+                                                                          const void *data, size_t size,
+                                                                          std::vector<const_data_buffer> &hashes) {
+  return impl_->generate_replicas(replicas, data, size, hashes);
+}
+
+expected<std::vector<const_data_buffer>> chunk_storage::regenerate_replicas(
+    const std::unordered_map<uint16_t, const_data_buffer> &horcruxes, const std::vector<uint16_t> &targets) {
+  return impl_->regenerate_replicas(horcruxes, targets);
 }
 
 expected<const_data_buffer> chunk_storage::restore_data(

@@ -25,6 +25,18 @@ class chunk_storage {
   expected<std::vector<const_data_buffer>> generate_replicas(const std::vector<uint16_t> &replicas,
                                                              const void *data, size_t size);
 
+  // generate_replicas plus each replica's SHA-256 name (the replica_hash of
+  // dht_network_client.cpp:79 / :593), computed on the device.
+  expected<std::vector<const_data_buffer>> generate_replicas(const std::vector<uint16_t> &replicas,
+                                                             const void *data, size_t size,
+                                                             std::vector<const_data_buffer> &hashes);
+
+  // Repair without materialising the object (sync_process.cpp:313-335 does
+  // restore_data + generate_replica): replicas `targets` from exactly
+  // min_horcrux equal-size horcruxes, byte-identical to that route.
+  expected<std::vector<const_data_buffer>> regenerate_replicas(
+      const std::unordered_map<uint16_t, const_data_buffer> &horcruxes, const std::vector<uint16_t> &targets);
+
  private:
   friend class ichunk_storage;
   _chunk_storage *const impl_;

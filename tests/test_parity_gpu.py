@@ -155,6 +155,38 @@ def test_batched_objects_with_strides(ec):
             assert np.array_equal(out[r, o].cpu().numpy(), O.encode(k, r, d))
 
 
+@pytest.mark.parametrize("k,n,size,count,pad", [
+    (32, 64, 65536, 5, 0),       # the live shape (dht_network.h:22-25): tiles straddle objects
+    (32, 64, 65536, 3, 2),       # 4-byte-aligned replica stride
+    (16, 20, 12288, 11, 0),      # 3 groups per object, stream tail in the middle of object 10
+    (16, 20, 12288 + 7, 6, 0),   # + a partial last stripe per object
+    (32, 40, 4 * 8192, 9, 6),
+    (16, 20, 2 * 65536 + 1000, 3, 0),  # F % 128 != 0: whole tiles per object, generic rest
+])
+def test_fast_encode_object_stream(ec, k, n, size, count, pad):
+    """Batches of small objects ride the bit-sliced kernel as one stripe
+    stream (tiles cross object boundaries); every replica byte, trailer
+    included, equals the oracle's, and nothing is written past a replica."""
+    import torch
+    from vds_amd import chunk
+    L = chunk.replica_size(k, size)
+    stride = size + 16
+    t = torch.empty(stride * count, dtype=torch.uint8, device="cuda")
+    for o in range(count):
+        chunk.fill_splitmix_device(t[o * stride:], size, SEED + 900 + o)
+    out = torch.zeros((n, count, L + pad), dtype=torch.uint8, device="cuda")
+    chunk.encode_device(k, list(range(n)), t, size, stride, count, [out[i].data_ptr() for i in range(n)], L + pad)
+    torch.cuda.synchronize()
+    host = out.cpu().numpy()
+    assert chunk._lib.lib().vds_ec_encode16_path(k, np.arange(n, dtype=np.uint16).ctypes.data_as(chunk._lib.u16p),
+                                                  n, size) == 2
+    for o in range(count):
+        d = O.splitmix(SEED + 900 + o, size)
+        for r in range(n):
+            assert np.array_equal(host[r, o, :L], O.encode(k, r, d)), f"object {o} replica {r}"
+            assert not host[r, o, L:].any()
+
+
 # ------------------------------------------------------------------ restore
 
 @pytest.mark.parametrize("entry", G["restore16"], ids=lambda e: f"k{e['k']}s{e['size']}")

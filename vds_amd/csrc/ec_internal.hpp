@@ -57,11 +57,14 @@ struct GenericRestoreArgs {
   uint64_t out_len;  // bytes of the restored object (trim bound)
 };
 
+// Bit-sliced encode: the full stripes of `count` objects, F = 128
+// groups_per_obj per object, as one stream of 2048-stripe tiles (k >= 8:
+// tiles may straddle objects; k = 4: groups_per_obj % 16 == 0).
 struct FastEncodeArgs {
   const uint8_t *in;
   uint64_t in_stride;
   uint64_t out_stride;
-  uint32_t tiles_per_obj;
+  uint32_t groups_per_obj;
   uint32_t total_tiles;
   uint8_t *outs[kMaxLaunchReplicas];  // outs[r] for replica id r = 0..N-1
 };

@@ -138,11 +138,6 @@ constexpr int popcount32(uint32_t v) {
 }
 
 
-#ifndef VDS_ENC_MAP  // slot -> stripe map of the encode tile (k = 16, 32):
-#define VDS_ENC_MAP 3   //  0: stripe s + 64 i (2-byte stores), 1: contiguous 1 KiB loads + 4-byte
-#endif                  //  stores, 2: paired half-line loads + 8-byte full-line stores, 3: slots
-                        //  (j, 16+j) of set s = stripes 2s + 128j (+1): 1 KiB loads, 256 B stores
-
 // VALU cost of one row-form Horner step for replica r (bitslice.hpp): used
 // to balance replicas across waves.
 constexpr int horner_cost(int r) { return r == 0 ? 1 : row_horner_cost((uint32_t)r); }
@@ -197,7 +192,7 @@ struct EncodeShape {
   static constexpr int kPlaneBytes = 64 * kSetWords * 4;
   static constexpr int kLdsBytes = kPlaneBytes;
   static constexpr int kWavesPerSimd = 2;  // 256 VGPRs: accumulators ping-pong + the prefetched tile
-  static constexpr int kMap = kLanesPerSet >= 2 ? VDS_ENC_MAP : 0;
+  static constexpr int kMap = kLanesPerSet >= 2 ? 3 : 0;  // slot map (store_replica_groups); k = 4: 0
   static constexpr ReplicaPlan<N, kWaves, RPW> kPlan = plan_replicas<N, kWaves, RPW>();
   static_assert(K % 4 == 0 && WV == K / 4, "fast encode: k % 4 == 0 and k/4 waves");
   static_assert(RPW * WV >= N, "every replica needs a wave");
@@ -272,49 +267,64 @@ __device__ __forceinline__ void rows_step(Plane16 (&dst)[PR], const Plane16 (&sr
   }(std::make_index_sequence<PR>{});
 }
 
-// Store replica r's cells of this tile: `tile_off` is the tile's byte offset
-// in every replica, `lane_off` = 2 * lane the lane's own cell.
+// Where a tile's cells live.  The batch is one stream of count x F full
+// stripes (F = 128 groups_per_obj): group j (128 stripes) of tile t is global
+// group 16 t + j, i.e. group q of object o = (16 t + j) / groups_per_obj.  A
+// group never straddles two objects, but a tile may (the live production
+// shape: k = 32, 64 KiB objects = 8 groups).
+struct TilePos {
+  uint32_t o, q;  // object and group-in-object of the tile's first group (wave-uniform)
+};
 
+__device__ __forceinline__ TilePos tile_pos(const FastEncodeArgs &a, uint32_t tile) {
+  const uint32_t g = 16u * tile;
+  const uint32_t o = g / a.groups_per_obj;
+  return TilePos{o, g - o * a.groups_per_obj};
+}
 
-// Map 1/2 stores.  Set s = SPW w + t (SPW = sets per transposing wave).  Slot
-// q < 16 and slot 16 + q hold adjacent stripes, so output word q (low half =
-// slot q, high half = slot 16 + q, transpose16x2) is 4 contiguous bytes.
-//  map 1: slot q -> stripe 32 SPW w + 2 SPW q + 2 t: word q at byte 64 SPW w + 4 SPW q + 4 t
-//  map 2: slot 8h + r -> stripe 32 SPW w + 4 SPW r + 4 t + 2 h: words r and 8 + r are
-//         4 consecutive stripes, one 8-byte store at 64 SPW w + 8 SPW r + 8 t; a
-//         wave-instruction writes SPW/2... whole 128-byte lines.
-template <int SPW, int MAP>
-__device__ __forceinline__ void store_replica_mapped(const Plane16 &acc, uint8_t *tile, int lane, const BitMasks &bm) {
+// Map 3 (k >= 8): slots j and 16 + j of set s hold stripes 2s + 128j and
+// 2s + 128j + 1, so output word j (low half = slot j, high half = slot 16 + j,
+// transpose16x2) is the 4 bytes of stripes 2s, 2s+1 of group j: one dword
+// store per word, 256 contiguous bytes per wave-instruction.
+template <bool STREAM>
+__device__ __forceinline__ void store_replica_groups(const Plane16 &acc, uint8_t *rep, const FastEncodeArgs &a,
+                                                     TilePos tp, int lane, const BitMasks &bm) {
   uint32_t rows[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) rows[j] = acc.p[j ^ 8];  // word bit j <-> cell bit j^8 (BE)
   transpose16x2(rows, bm);
-  const int w = lane / SPW, t = lane % SPW;
-  if constexpr (MAP == 3) {
-    uint8_t *b = tile + 4 * lane;
+#if VDS_DIAG_ENC == 3
+  if (tp.o != 0xFFFFFFFFu) return;  // transposes kept, stores never run
+#endif
+  // (replica strides L = 2T + 2 leave odd objects 2-byte aligned: gfx950
+  // global stores need no natural alignment, tested by the strided batches)
+  if constexpr (!STREAM) {  // whole tiles per object: one base, immediate offsets
+    uint32_t *b = reinterpret_cast<uint32_t *>(rep + (uint64_t)tp.o * a.out_stride + 256u * tp.q + 4 * lane);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) *reinterpret_cast<uint32_t *>(b + 256 * q) = rows[q];
-  } else if constexpr (MAP == 1) {
-    uint8_t *b = tile + 64 * SPW * w + 4 * t;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) *reinterpret_cast<uint32_t *>(b + 4 * SPW * q) = rows[q];
+    for (int j = 0; j < 16; ++j) b[64 * j] = rows[j];
   } else {
-    uint8_t *b = tile + 64 * SPW * w + 8 * t;
+    uint32_t o = tp.o, q = tp.q;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) *reinterpret_cast<u32x2 *>(b + 8 * SPW * r) = u32x2{rows[r], rows[8 + r]};
+    for (int j = 0; j < 16; ++j) {
+      *reinterpret_cast<uint32_t *>(rep + (uint64_t)o * a.out_stride + 256u * q + 4 * lane) = rows[j];
+      if (++q == a.groups_per_obj) {
+        q = 0;
+        ++o;
+      }
+    }
   }
 }
 
-template <int SPW, int MAP>
-__device__ __forceinline__ void store_rep(const Plane16 &acc, uint8_t *rep, uint64_t tile_off, lds_stage *, int lane,
-                                          const BitMasks &bm) {
+template <int MAP, bool STREAM>
+__device__ __forceinline__ void store_rep(const Plane16 &acc, uint8_t *rep, const FastEncodeArgs &a, TilePos tp,
+                                          int lane, const BitMasks &bm) {
 #if VDS_DIAG_ENC == 1
-  if (tile_off != 1) return;  // never stores for real tiles (offsets are even)
+  if (tp.o != 0xFFFFFFFFu) return;  // never stores
 #endif
-  if constexpr (MAP == 0)
-    store_replica(acc, rep + tile_off + 2 * lane, bm);
+  if constexpr (MAP == 0)  // k = 4: whole tiles of one object
+    store_replica(acc, rep + (uint64_t)tp.o * a.out_stride + 256u * tp.q + 2 * lane, bm);
   else
-    store_replica_mapped<SPW, MAP>(acc, rep + tile_off, lane, bm);
+    store_replica_groups<STREAM>(acc, rep, a, tp, lane, bm);
 }
 
 #ifndef VDS_ENC_PASS  // replicas evaluated per pass over the tile's cells
@@ -326,9 +336,9 @@ __device__ __forceinline__ void store_rep(const Plane16 &acc, uint8_t *rep, uint
 // between A and B and the loop carries no register copies.  Splitting a
 // wave's replicas into passes spreads its stores over the tile instead of
 // one burst at the end (the kernel is write-bound when they bunch up).
-template <int K, int N, int RPW, int WV, int W, int S0, int PR>
-__device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const FastEncodeArgs &a, uint64_t tile_off,
-                                            lds_stage *stage, int lane, const BitMasks &bm) {
+template <int K, int N, int RPW, int WV, int W, int S0, int PR, bool ST>
+__device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const FastEncodeArgs &a, TilePos tp, int lane,
+                                            const BitMasks &bm) {
   using S = EncodeShape<K, N, RPW, WV>;
   constexpr bool kAnyHorner = [] {
     for (int s = S0; s < S0 + PR && s < RPW; ++s)
@@ -339,8 +349,7 @@ __device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const Fa
 #pragma unroll
     for (int s = S0; s < S0 + PR && s < RPW; ++s)
       if (S::kPlan.rep[W][s] == 0)
-        store_rep<S::kSetsPerWave, S::kMap>(lds_planes(set_planes + S::cell_off(0)), a.outs[0], tile_off, stage, lane,
-                                            bm);
+        store_rep<S::kMap, ST>(lds_planes(set_planes + S::cell_off(0)), a.outs[0], a, tp, lane, bm);
     return;
   }
   Plane16 A[PR], B[PR];
@@ -361,100 +370,90 @@ __device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const Fa
 #pragma unroll
   for (int s = 0; s < PR; ++s) {
     const int r = S0 + s < RPW ? S::kPlan.rep[W][S0 + s] : -1;
-    if (r == 0) store_rep<S::kSetsPerWave, S::kMap>(xa, a.outs[0], tile_off, stage, lane, bm);
-    if (r > 0) store_rep<S::kSetsPerWave, S::kMap>(A[s], a.outs[r], tile_off, stage, lane, bm);
+    if (r == 0) store_rep<S::kMap, ST>(xa, a.outs[0], a, tp, lane, bm);
+    if (r > 0) store_rep<S::kMap, ST>(A[s], a.outs[r], a, tp, lane, bm);
   }
 }
 
-template <int K, int N, int RPW, int WV, int W, int S0 = 0>
-__device__ __forceinline__ void encode_wave_group(const uint32_t *set_planes, const FastEncodeArgs &a,
-                                                  uint64_t tile_off, lds_stage *stage, int lane, const BitMasks &bm) {
+template <int K, int N, int RPW, int WV, int W, bool ST, int S0 = 0>
+__device__ __forceinline__ void encode_wave_group(const uint32_t *set_planes, const FastEncodeArgs &a, TilePos tp,
+                                                  int lane, const BitMasks &bm) {
   constexpr int PR = VDS_ENC_PASS < RPW ? VDS_ENC_PASS : RPW;
   if constexpr (S0 < RPW) {
-    encode_pass<K, N, RPW, WV, W, S0, PR>(set_planes, a, tile_off, stage, lane, bm);
-    encode_wave_group<K, N, RPW, WV, W, S0 + PR>(set_planes, a, tile_off, stage, lane, bm);
+    encode_pass<K, N, RPW, WV, W, S0, PR, ST>(set_planes, a, tp, lane, bm);
+    encode_wave_group<K, N, RPW, WV, W, ST, S0 + PR>(set_planes, a, tp, lane, bm);
   }
 }
 
-template <int K, int N, int RPW, int WV, int W>
-__device__ __forceinline__ void encode_dispatch(int wave, const uint32_t *set_planes, const FastEncodeArgs &a,
-                                                uint64_t tile_off, lds_stage *stage, int lane, const BitMasks &bm) {
+template <int K, int N, int RPW, int WV, bool ST, int W>
+__device__ __forceinline__ void encode_dispatch(int wave, const uint32_t *set_planes, const FastEncodeArgs &a, TilePos tp,
+                                                int lane, const BitMasks &bm) {
   using S = EncodeShape<K, N, RPW, WV>;
   if constexpr (W < S::kWaves) {
     if (wave == W)
-      encode_wave_group<K, N, RPW, WV, W>(set_planes, a, tile_off, stage, lane, bm);
+      encode_wave_group<K, N, RPW, WV, W, ST>(set_planes, a, tp, lane, bm);
     else
-      encode_dispatch<K, N, RPW, WV, W + 1>(wave, set_planes, a, tile_off, stage, lane, bm);
+      encode_dispatch<K, N, RPW, WV, ST, W + 1>(wave, set_planes, a, tp, lane, bm);
   }
 }
 
-// Load dwords 2p, 2p+1 of the 32 stripes of set `set` of `tile`: slot i of a
-// set s <-> stripe stripe0 + s + 64 i.  The data stays in the loaded vector
-// registers until the next iteration unpacks it, so no copy forces an early
-// s_waitcnt.
-
+// k = 4: load dwords 2p, 2p+1 of the 32 stripes of set `set`; slot i <->
+// stripe stripe0 + s + 64 i (whole tiles of one object).  The data stays in
+// the loaded vector registers until the next iteration unpacks it, so no copy
+// forces an early s_waitcnt.
 template <int K>
 __device__ __forceinline__ void encode_load(u32x2 (&P)[32], const FastEncodeArgs &a, uint32_t tile, int set, int p) {
-  const uint32_t o = tile / a.tiles_per_obj;
-  const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
-  const uint8_t *src = a.in + (uint64_t)o * a.in_stride + (stripe0 + set) * (2 * K) + 8 * p;
+  const TilePos tp = tile_pos(a, tile);
+  const uint8_t *src = a.in + (uint64_t)tp.o * a.in_stride + ((uint64_t)128 * tp.q + set) * (2 * K) + 8 * p;
 #pragma unroll
   for (int i = 0; i < 32; ++i) P[i] = *reinterpret_cast<const u32x2 *>(src + (uint64_t)i * 64 * (2 * K));
 }
 
-// 16-byte loads (K/4 >= 2 lanes per set): the lanes of an adjacent pair (same
-// set, p = 2u + par) each load one whole 16-byte chunk u of a stripe -- par 0
-// the stripe of slot 2m, par 1 that of slot 2m+1 -- and swap halves with
-// one DPP quad_perm, so every lane ends with dwords 2p, 2p+1 of both
-// stripes.  A wave-load then reads two runs of 512 contiguous bytes with 16
-// bytes per lane, against one run with 8 bytes per lane for encode_load
-// (measured 15% faster for the same bytes).
-template <int K, int MAP>
+// k >= 8: 16-byte pair loads.  The lanes of an adjacent pair (same set, p =
+// 2u + par) each load one whole 16-byte chunk u -- par 0 of stripe 2s + 128j
+// (slot j), par 1 of stripe 2s + 128j + 1 (slot 16 + j) -- and swap halves
+// with one DPP quad_perm, so every lane ends with dwords 2p, 2p+1 of both.  A
+// wave-load reads 256/k * 2 whole stripes = 1 KiB contiguous, 16 B per lane.
+template <int K, bool STREAM>
 __device__ __forceinline__ void encode_load16(u32x4 (&V)[16], const FastEncodeArgs &a, uint32_t tile, int set, int p) {
-  constexpr int SPW = 256 / K;  // sets per transposing wave
-  const uint32_t o = tile / a.tiles_per_obj;
-  const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
-  const uint8_t *obj = a.in + (uint64_t)o * a.in_stride + 16 * (p >> 1);
-  if constexpr (MAP == 0) {  // pair m = slots (2m, 2m+1) = stripes set + 128 m (+64)
-    const uint8_t *src = obj + (stripe0 + set + 64 * (p & 1)) * (2 * K);
+  const TilePos tp = tile_pos(a, tile);
+  const uint64_t lane_off = (uint64_t)(2 * set + (p & 1)) * (2 * K) + 16 * (p >> 1);
+  uint32_t o = tp.o, q = tp.q;
+  if constexpr (!STREAM) {  // whole tiles per object
+    const uint8_t *src = a.in + (uint64_t)o * a.in_stride + (uint64_t)q * 128 * (2 * K) + lane_off;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) V[m] = *reinterpret_cast<const u32x4 *>(src + (uint64_t)m * 128 * (2 * K));
-  } else {  // pair j = slots (j, 16 + j) = stripes A and A + 1 (maps 1, 2 above store_replica_mapped)
-    const int w = set / SPW, t = set % SPW;
-    const uint8_t *src =
-        MAP == 3 ? obj + (stripe0 + 2 * set + (p & 1)) * (2 * K)
-                 : obj + (stripe0 + 32 * SPW * w + (MAP == 1 ? 2 : 4) * t + (p & 1)) * (2 * K);
+    for (int j = 0; j < 16; ++j) V[j] = *reinterpret_cast<const u32x4 *>(src + (uint64_t)j * 128 * (2 * K));
+    return;
+  }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int step = MAP == 3 ? 128 * j : MAP == 1 ? 2 * SPW * j : 4 * SPW * (j % 8) + 2 * (j / 8);
-      V[j] = *reinterpret_cast<const u32x4 *>(src + (uint64_t)step * (2 * K));
+  for (int j = 0; j < 16; ++j) {
+    V[j] = *reinterpret_cast<const u32x4 *>(a.in + (uint64_t)o * a.in_stride + (uint64_t)q * 128 * (2 * K) + lane_off);
+    if (++q == a.groups_per_obj) {
+      q = 0;
+      ++o;
     }
   }
 }
 
-// R[g][i] = dword 2p + g of slot i's stripe, from the loaded chunks: pair m
-// holds slots (lo, hi) = (2m, 2m+1) for map 0 and (m, 16 + m) for maps 1, 2.
-template <int MAP>
+// R[g][i] = dword 2p + g of slot i's stripe, from the loaded chunks (pair j
+// holds slots j and 16 + j).
 __device__ __forceinline__ void encode_unpack16(const u32x4 (&V)[16], uint32_t (&R)[2][32], bool par) {
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
-    const int lo = MAP == 0 ? 2 * m : m, hi = MAP == 0 ? 2 * m + 1 : 16 + m;
     const u32x4 v = V[m];
     const uint32_t s0 = par ? v.x : v.z, s1 = par ? v.y : v.w;   // the partner's half
     const uint32_t r0 = __builtin_amdgcn_mov_dpp(s0, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
     const uint32_t r1 = __builtin_amdgcn_mov_dpp(s1, 0xB1, 0xF, 0xF, false);
-    R[0][lo] = par ? r0 : v.x;
-    R[1][lo] = par ? r1 : v.y;
-    R[0][hi] = par ? v.z : r0;
-    R[1][hi] = par ? v.w : r1;
+    R[0][m] = par ? r0 : v.x;
+    R[1][m] = par ? r1 : v.y;
+    R[0][16 + m] = par ? v.z : r0;
+    R[1][16 + m] = par ? v.w : r1;
   }
 }
 
-#ifndef VDS_ENC_LOAD16  // 1: 16-byte pair loads + DPP swap (k >= 8); 0: 8-byte loads
-#define VDS_ENC_LOAD16 1
-#endif
-
-template <int K, int N, int RPW, int WV>
+// STREAM: tiles may straddle objects (groups_per_obj % 16 != 0, k >= 8); the
+// non-stream instantiation keeps one base address per tile.
+template <int K, int N, int RPW, int WV, bool STREAM>
 __global__ __launch_bounds__((EncodeShape<K, N, RPW, WV>::kThreads), (EncodeShape<K, N, RPW, WV>::kWavesPerSimd))
 void k_encode_bs(FastEncodeArgs a) {
   using S = EncodeShape<K, N, RPW, WV>;
@@ -466,16 +465,15 @@ void k_encode_bs(FastEncodeArgs a) {
   const int tp = lane % S::kLanesPerSet;
   uint32_t *t_planes = lds + tset * S::kSetWords + S::cell_off(4 * tp);
   const uint32_t *my_set = lds + lane * S::kSetWords;
-  lds_stage *stage = nullptr;  // (store staging through LDS measured slower: 2-byte stores are not the limit)
   const BitMasks bm = bit_masks();
 
-  constexpr bool kLoad16 = VDS_ENC_LOAD16 && S::kLanesPerSet >= 2;
+  constexpr bool kLoad16 = S::kMap != 0;
   u32x2 P[kLoad16 ? 1 : 32];
   u32x4 V[kLoad16 ? 16 : 1];
   const bool par = (lane & 1) != 0;
   auto load = [&](uint32_t t) {
     if constexpr (kLoad16)
-      encode_load16<K, S::kMap>(V, a, t, tset, tp);
+      encode_load16<K, STREAM>(V, a, t, tset, tp);
     else
       encode_load<K>(P, a, t, tset, tp);
   };
@@ -485,7 +483,7 @@ void k_encode_bs(FastEncodeArgs a) {
     // ---- transpose to planes and publish in LDS: cell 4p+2g+h, bit b = R[g][16h + (b^8)]
     uint32_t R[2][32];
     if constexpr (kLoad16) {
-      encode_unpack16<S::kMap>(V, R, par);
+      encode_unpack16(V, R, par);
     } else {
 #pragma unroll
       for (int i = 0; i < 32; ++i) {
@@ -510,10 +508,7 @@ void k_encode_bs(FastEncodeArgs a) {
     const uint32_t next = tile + gridDim.x;
     if (next < a.total_tiles) load(next);
     // ---- evaluate this wave's replicas and store
-    const uint32_t o = tile / a.tiles_per_obj;
-    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
-    const uint64_t tile_off = (uint64_t)o * a.out_stride + 2 * stripe0;
-    encode_dispatch<K, N, RPW, WV, 0>(wave, my_set, a, tile_off, stage, lane, bm);
+    encode_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
     __syncthreads();
   }
 }
@@ -1096,12 +1091,12 @@ hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int K, int N, int RPW, int WV>
-static hipError_t launch_encode_bs(const FastEncodeArgs &a, hipStream_t s) {
+template <int K, int N, int RPW, int WV, bool STREAM>
+static hipError_t launch_encode_bs_st(const FastEncodeArgs &a, hipStream_t s) {
   using S = EncodeShape<K, N, RPW, WV>;
   static bool configured = false;
   if (!configured) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_encode_bs<K, N, RPW, WV>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_encode_bs<K, N, RPW, WV, STREAM>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, S::kLdsBytes);
     if (e != hipSuccess) return e;
     configured = true;
@@ -1110,8 +1105,15 @@ static hipError_t launch_encode_bs(const FastEncodeArgs &a, hipStream_t s) {
   int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
   if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_encode_bs<K, N, RPW, WV>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  hipLaunchKernelGGL((k_encode_bs<K, N, RPW, WV, STREAM>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
   return hipGetLastError();
+}
+
+template <int K, int N, int RPW, int WV>
+static hipError_t launch_encode_bs(const FastEncodeArgs &a, hipStream_t s) {
+  if (a.groups_per_obj % 16 == 0) return launch_encode_bs_st<K, N, RPW, WV, false>(a, s);
+  if constexpr (K >= 8) return launch_encode_bs_st<K, N, RPW, WV, true>(a, s);
+  return hipErrorNotSupported;
 }
 
 #ifndef VDS_ENC16_RPW  // replicas per wave / waves of the k=16, n=20 encode
@@ -1120,12 +1122,13 @@ static hipError_t launch_encode_bs(const FastEncodeArgs &a, hipStream_t s) {
 #endif
 
 bool has_encode_fast(uint32_t k, uint32_t n) {
-  return (k == 16 && n == 20) || (k == 32 && n == 40) || (k == 4 && n == 6);
+  return (k == 16 && n == 20) || (k == 32 && n == 40) || (k == 32 && n == 64) || (k == 4 && n == 6);
 }
 
 hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, hipStream_t s) {
   if (k == 16 && n == 20) return launch_encode_bs<16, 20, VDS_ENC16_RPW, VDS_ENC16_WAVES>(a, s);
   if (k == 32 && n == 40) return launch_encode_bs<32, 40, 5, 8>(a, s);
+  if (k == 32 && n == 64) return launch_encode_bs<32, 64, 8, 8>(a, s);  // the live shape (dht_network.h:22-25)
   if (k == 4 && n == 6) return launch_encode_bs<4, 6, 6, 1>(a, s);
   return hipErrorNotSupported;
 }

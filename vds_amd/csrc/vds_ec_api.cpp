@@ -165,49 +165,72 @@ int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n,
   const uint64_t stripe_bytes = (uint64_t)k * cb;
   const uint64_t T = (size + stripe_bytes - 1) / stripe_bytes;
 
-  // Bit-sliced path: 16-bit byte-API cells, replicas exactly 0..n-1.
-  uint64_t fast_stripes = 0;
+  // Bit-sliced path: 16-bit byte-API cells, replicas exactly 0..n-1.  It
+  // covers the first gpo 128-stripe groups of every object, taken as one
+  // stream of 2048-stripe tiles: with F = full stripes per object, gpo = F/128
+  // when 128 | F (tiles may straddle objects, k >= 8), else gpo = 16 floor(F/2048)
+  // (whole tiles per object).  The rest is generic.
+  const uint64_t F = size / stripe_bytes;  // stripes with no zero padding
+  uint64_t gpo = 0, fast_groups = 0;
   bool contiguous = true;
   for (uint32_t i = 0; i < n; ++i) contiguous &= (replicas[i] == i);
-  if (cb == 2 && !cells && contiguous && has_encode_fast(k, n)) {
-    const uint64_t full = size / stripe_bytes;  // stripes with no zero padding
-    const uint64_t tiles = full / kTileStripes;
-    const uint64_t total = tiles * count;
-    if (tiles > 0 && total <= 0xFFFFFFFFull) {
+  if (cb == 2 && !cells && contiguous && has_encode_fast(k, n) && ((uintptr_t)in | in_stride) % 4 == 0) {
+    if (F % 128 == 0 && (k >= 8 || F % kTileStripes == 0))
+      gpo = F / 128;
+    else
+      gpo = 16 * (F / kTileStripes);
+    const uint64_t total = gpo * count / 16;
+    if (gpo > 0 && gpo <= 0xFFFFFFFFull && total > 0 && total <= 0xFFFFFFFFull) {
       FastEncodeArgs fa{};
       fa.in = in;
       fa.in_stride = in_stride;
       fa.out_stride = out_stride;
-      fa.tiles_per_obj = (uint32_t)tiles;
+      fa.groups_per_obj = (uint32_t)gpo;
       fa.total_tiles = (uint32_t)total;
       for (uint32_t i = 0; i < n; ++i) fa.outs[i] = outs[i];
       hipError_t e = launch_encode_fast(k, n, fa, s);
       if (e != hipSuccess) return hip_status(e);
-      fast_stripes = tiles * kTileStripes;
+      fast_groups = total * 16;
     }
   }
-  // Generic path for the rest (+ trailers), in launches of <= 64 replicas.
-  for (uint32_t base = 0; base < n; base += kMaxLaunchReplicas) {
-    GenericEncodeArgs ga{};
-    ga.in = in;
-    ga.size = size;
-    ga.in_stride = in_stride;
-    ga.count = count;
-    ga.k = k;
-    ga.cell_bytes = cb;
-    ga.flags = flags;
-    ga.nrep = (n - base) < (uint32_t)kMaxLaunchReplicas ? (n - base) : (uint32_t)kMaxLaunchReplicas;
-    ga.t_begin = fast_stripes;
-    ga.t_count = T - fast_stripes;
-    ga.stripes = T;
-    ga.write_trailer = trailer ? 1 : 0;
-    ga.out_stride = out_stride;
-    for (uint32_t i = 0; i < ga.nrep; ++i) {
-      ga.nodes[i] = replicas[base + i];
-      ga.outs[i] = outs[base + i];
+  // Generic path for the rest (+ trailers), in launches of <= 64 replicas:
+  // objects [0, o_full) need only their partial stripe and trailer, object
+  // o_full its uncovered tail, objects after it everything.
+  const uint64_t o_full = fast_groups ? fast_groups / gpo : 0;
+  struct Part {
+    uint64_t o0, cnt, t_begin;
+  };
+  Part parts[3] = {{0, o_full, 128 * gpo},
+                   {o_full, o_full < count ? 1u : 0u, fast_groups ? 128 * (fast_groups - o_full * gpo) : 0},
+                   {o_full + 1, o_full + 1 < count ? count - o_full - 1 : 0, 0}};
+  if (!fast_groups) {
+    parts[0] = {0, count, 0};
+    parts[1].cnt = parts[2].cnt = 0;
+  }
+  for (const Part &pt : parts) {
+    if (pt.cnt == 0) continue;
+    for (uint32_t base = 0; base < n; base += kMaxLaunchReplicas) {
+      GenericEncodeArgs ga{};
+      ga.in = in + pt.o0 * in_stride;
+      ga.size = size;
+      ga.in_stride = in_stride;
+      ga.count = (uint32_t)pt.cnt;
+      ga.k = k;
+      ga.cell_bytes = cb;
+      ga.flags = flags;
+      ga.nrep = (n - base) < (uint32_t)kMaxLaunchReplicas ? (n - base) : (uint32_t)kMaxLaunchReplicas;
+      ga.t_begin = pt.t_begin;
+      ga.t_count = T - pt.t_begin;
+      ga.stripes = T;
+      ga.write_trailer = trailer ? 1 : 0;
+      ga.out_stride = out_stride;
+      for (uint32_t i = 0; i < ga.nrep; ++i) {
+        ga.nodes[i] = replicas[base + i];
+        ga.outs[i] = outs[base + i] + pt.o0 * out_stride;
+      }
+      hipError_t e = launch_encode_generic(ga, s);
+      if (e != hipSuccess) return hip_status(e);
     }
-    hipError_t e = launch_encode_generic(ga, s);
-    if (e != hipSuccess) return hip_status(e);
   }
   return VDS_EC_OK;
 }
@@ -1023,8 +1046,10 @@ int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void
 int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint64_t size) {
   bool contiguous = replicas != nullptr;
   for (uint32_t i = 0; contiguous && i < n; ++i) contiguous &= (replicas[i] == i);
-  const uint64_t tiles = k ? size / (2ull * k) / kTileStripes : 0;
-  return (contiguous && has_encode_fast(k, n) && tiles > 0) ? 2 : 1;
+  // (for a batch of at least one 2048-stripe tile of full stripes)
+  const uint64_t F = k ? size / (2ull * k) : 0;
+  const bool fast = F >= kTileStripes || (F > 0 && F % 128 == 0 && k >= 8);
+  return (contiguous && has_encode_fast(k, n) && fast) ? 2 : 1;
 }
 
 int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size) {

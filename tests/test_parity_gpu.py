@@ -189,6 +189,31 @@ def test_fast_encode_object_stream(ec, k, n, size, count, pad):
 
 # ------------------------------------------------------------------ restore
 
+@pytest.mark.parametrize("k,nodes,size,count", [
+    (32, list(range(1, 64, 2)), 65536, 5),                 # live shape: 2 groups per object, tiles straddle
+    (16, list(range(20, 36)), 16384, 7),                   # runtime-coefficient kernel, 1 group per object
+    (16, list(range(20, 36)), 3 * 16384 + 9, 4),          # + a partial stripe (generic tail per object)
+    (32, list(range(8, 40)), 2 * 131072 + 64 * 512, 3),   # whole tiles + a stream of groups
+])
+def test_fast_restore_object_stream(ec, k, nodes, size, count):
+    """Batches of small objects on the bit-sliced runtime-coefficient restore
+    (512-stripe groups, tiles across object boundaries) plus the generic
+    remainder: every object comes back bit-exact, nothing written past it."""
+    import torch
+    from vds_amd import chunk
+    L = chunk.replica_size(k, size)
+    objs = [O.splitmix(SEED + 1300 + o, size) for o in range(count)]
+    reps = np.stack([np.stack([O.encode(k, r, d) for d in objs]) for r in nodes])  # (k, count, L)
+    dev = torch.from_numpy(reps).cuda()
+    out = torch.zeros((count, size + 64), dtype=torch.uint8, device="cuda")
+    chunk.restore_device(k, nodes, [dev[j].data_ptr() for j in range(k)], L, L, size % (2 * k), count, out, size + 64)
+    torch.cuda.synchronize()
+    host = out.cpu().numpy()
+    for o in range(count):
+        assert np.array_equal(host[o, :size], objs[o]), f"object {o}"
+        assert not host[o, size:].any()
+
+
 @pytest.mark.parametrize("entry", G["restore16"], ids=lambda e: f"k{e['k']}s{e['size']}")
 def test_restore_golden(ec, entry):
     k, size = entry["k"], entry["size"]

@@ -69,12 +69,14 @@ struct FastEncodeArgs {
   uint8_t *outs[kMaxLaunchReplicas];  // outs[r] for replica id r = 0..N-1
 };
 
+// Bit-sliced runtime-coefficient restore over 512-stripe groups: the first
+// groups_per_obj groups of every object as one stream of 4-group tiles.
 struct FastRestoreArgs {
   const uint8_t *chunks[kMaxFastK];
   uint64_t chunk_stride;
   uint8_t *out;
   uint64_t out_stride;
-  uint32_t tiles_per_obj;
+  uint32_t groups_per_obj;
   uint32_t total_tiles;
   // k x k inverse, row-major, two coefficients per dword (low half = even
   // column) so the wave-uniform reads are scalar s_load_dword.

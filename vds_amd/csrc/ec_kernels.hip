@@ -531,21 +531,31 @@ __device__ __forceinline__ uint64_t restore_slot_stripe(int lane, int slot) {
   return 8u * lane + 512u * (slot >> 3) + (slot & 7);
 }
 
-template <int K>
+// Tiles in 512-stripe groups (1 KiB of every survivor): group q of tile t is
+// global group 4 t + q = group r of object o (groups_per_obj per object).
+// STREAM: tiles may straddle objects (small objects, groups_per_obj % 4 != 0).
+__device__ __forceinline__ void restore_group(const FastRestoreArgs &a, uint32_t tile, uint32_t q, uint32_t &o,
+                                              uint32_t &r) {
+  const uint32_t g = 4u * tile + q;
+  o = g / a.groups_per_obj;
+  r = g - o * a.groups_per_obj;
+}
+
+template <int K, bool STREAM>
 __device__ __forceinline__ void restore_load(u32x4 (&Q)[RestoreShape<K>::kPerWave][4], const FastRestoreArgs &a,
                                              uint32_t tile, int lane, int wave) {
   using S = RestoreShape<K>;
-  const uint32_t o = tile / a.tiles_per_obj;
-  const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
 #pragma unroll
-  for (int s = 0; s < S::kPerWave; ++s) {
-    const uint8_t *src = a.chunks[wave * S::kPerWave + s] + (uint64_t)o * a.chunk_stride + 2 * stripe0 + 16 * lane;
+  for (int q = 0; q < 4; ++q) {
+    uint32_t o, r;
+    restore_group(a, tile, STREAM ? q : 0, o, r);
+    const uint64_t off = (uint64_t)o * a.chunk_stride + 1024ull * (STREAM ? r : r + q) + 16 * lane;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) Q[s][q] = *reinterpret_cast<const u32x4 *>(src + 1024 * q);
+    for (int s = 0; s < S::kPerWave; ++s) Q[s][q] = *reinterpret_cast<const u32x4 *>(a.chunks[wave * S::kPerWave + s] + off);
   }
 }
 
-template <int K>
+template <int K, bool STREAM>
 __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(FastRestoreArgs a) {
   using S = RestoreShape<K>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -555,7 +565,7 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
 
   u32x4 Q[S::kPerWave][4];
   uint32_t tile = blockIdx.x;
-  if (tile < a.total_tiles) restore_load<K>(Q, a, tile, lane, wave);
+  if (tile < a.total_tiles) restore_load<K, STREAM>(Q, a, tile, lane, wave);
   for (; tile < a.total_tiles; tile += gridDim.x) {
     uint32_t W[S::kPerWave][16];
 #pragma unroll
@@ -576,7 +586,7 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
     }
     __syncthreads();
     const uint32_t next = tile + gridDim.x;
-    if (next < a.total_tiles) restore_load<K>(Q, a, next, lane, wave);
+    if (next < a.total_tiles) restore_load<K, STREAM>(Q, a, next, lane, wave);
     // ---- outputs m = wave*kPerWave + s : sum_j M[m][j] * Y_j
     Plane16 acc[S::kPerWave];
 #pragma unroll
@@ -595,9 +605,6 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
       plane_mac_rt<S::kPerWave>(acc, y, c);
     }
     // ---- back to big-endian cells: word group w' = cells (2w', 2w'+1)
-    const uint32_t o = tile / a.tiles_per_obj;
-    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
-    uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
 #pragma unroll
     for (int g = 0; g < S::kPerWave / 2; ++g) {
       uint32_t rows[32];
@@ -607,11 +614,14 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
         for (int jb = 0; jb < 16; ++jb) rows[16 * h + jb] = acc[2 * g + h].p[jb ^ 8];
       transpose32(rows);
       const int wg = (wave * S::kPerWave) / 2 + g;
-      // slot 8q+e <-> stripe stripe0 + 8 lane + 512 q + e; plane bit pi <-> slot
-      // (pi < 16 ? 2 pi : 2 (pi-16) + 1)
+      // slot 8q+e <-> stripe 8 lane + 512 q + e of the tile (group q); plane bit
+      // pi <-> slot (pi < 16 ? 2 pi : 2 (pi-16) + 1)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        uint8_t *base = dst + (stripe0 + 8u * lane + 512u * q) * (2 * K) + 4 * wg;
+        uint32_t o, r;
+        restore_group(a, tile, STREAM ? q : 0, o, r);
+        uint8_t *base = a.out + (uint64_t)o * a.out_stride + ((uint64_t)512 * (STREAM ? r : r + q) + 8u * lane) * (2 * K) +
+                        4 * wg;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int slot = 8 * q + e;
@@ -1133,12 +1143,12 @@ hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, h
   return hipErrorNotSupported;
 }
 
-template <int K>
+template <int K, bool STREAM>
 static hipError_t launch_restore_bs_k(const FastRestoreArgs &a, hipStream_t s) {
   using S = RestoreShape<K>;
   static bool configured = false;
   if (!configured) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_restore_bs<K>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_restore_bs<K, STREAM>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, S::kLdsBytes);
     if (e != hipSuccess) return e;
     configured = true;
@@ -1147,15 +1157,16 @@ static hipError_t launch_restore_bs_k(const FastRestoreArgs &a, hipStream_t s) {
   int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
   if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_restore_bs<K>, dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  hipLaunchKernelGGL((k_restore_bs<K, STREAM>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
   return hipGetLastError();
 }
 
 bool has_restore_fast(uint32_t k) { return k == 16 || k == 32; }
 
 hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t s) {
-  if (k == 16) return launch_restore_bs_k<16>(a, s);
-  if (k == 32) return launch_restore_bs_k<32>(a, s);
+  const bool stream = a.groups_per_obj % 4 != 0;
+  if (k == 16) return stream ? launch_restore_bs_k<16, true>(a, s) : launch_restore_bs_k<16, false>(a, s);
+  if (k == 32) return stream ? launch_restore_bs_k<32, true>(a, s) : launch_restore_bs_k<32, false>(a, s);
   return hipErrorNotSupported;
 }
 

@@ -260,12 +260,16 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_
   uint64_t need = (out_len + stripe_bytes - 1) / stripe_bytes;  // stripes that produce output
   if (need > cells_per_chunk) need = cells_per_chunk;
 
-  uint64_t fast_stripes = 0;
+  // The fast kernels cover the first `per_obj` stripes of every object (or,
+  // in stream mode, the first `fast_total` stripes of the batch taken as one
+  // stream of objects of F full output stripes each); the generic kernel the rest.
+  const uint64_t F = out_len / stripe_bytes;  // stripes whose k cells all land in the output
+  uint64_t per_obj = 0, fast_total = 0;       // fast stripes: per object (whole tiles) / stream
   SynRestoreArgs sa{};
   uint32_t syn_n = 0;
   const bool syn = cb == 2 && !cells && plan_restore_syn(k, nodes, sa, &syn_n);
   if (syn) {
-    const uint64_t tiles = (out_len / stripe_bytes) / kTileStripes;
+    const uint64_t tiles = F / kTileStripes;
     const uint64_t total = tiles * count;
     if (tiles > 0 && total <= 0xFFFFFFFFull) {
       for (uint32_t j = 0; j < k; ++j) sa.chunks[j] = chunks[j];
@@ -276,38 +280,50 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_
       sa.total_tiles = (uint32_t)total;
       hipError_t e = launch_restore_syn(k, syn_n, sa, s);
       if (e != hipSuccess) return hip_status(e);
-      fast_stripes = tiles * kTileStripes;
+      per_obj = tiles * kTileStripes;
     }
   } else if (cb == 2 && !cells && has_restore_fast(k)) {
-    const uint64_t full = out_len / stripe_bytes;
-    const uint64_t tiles = full / kTileStripes;
-    const uint64_t total = tiles * count;
-    if (tiles > 0 && total <= 0xFFFFFFFFull) {
+    // 512-stripe groups; tiles of 4 groups may straddle objects when 512 | F
+    const uint64_t gpo = F % 512 == 0 ? F / 512 : 4 * (F / kTileStripes);
+    const uint64_t total = gpo * count / 4;
+    if (gpo > 0 && gpo <= 0xFFFFFFFFull && total > 0 && total <= 0xFFFFFFFFull) {
       FastRestoreArgs fa{};
       for (uint32_t j = 0; j < k; ++j) fa.chunks[j] = chunks[j];
       fa.chunk_stride = chunk_stride;
       fa.out = out;
       fa.out_stride = out_stride;
-      fa.tiles_per_obj = (uint32_t)tiles;
+      fa.groups_per_obj = (uint32_t)gpo;
       fa.total_tiles = (uint32_t)total;
       for (uint32_t i = 0; i < k * k; ++i) fa.matrix2[i >> 1] |= uint32_t(matrix[i]) << (16 * (i & 1));
       hipError_t e = launch_restore_fast(k, fa, s);
       if (e != hipSuccess) return hip_status(e);
-      fast_stripes = tiles * kTileStripes;
+      if (gpo % 4 == 0)
+        per_obj = 512 * gpo;
+      else
+        fast_total = 512 * 4 * total;
     }
   }
-  if (need > fast_stripes) {
+  // generic remainder: [0, o_full) from per_obj (or F), object o_full from its
+  // covered prefix, objects after it from 0
+  struct Part {
+    uint64_t o0, cnt, t_begin;
+  };
+  Part parts[3] = {{0, count, per_obj}, {0, 0, 0}, {0, 0, 0}};
+  if (fast_total) {
+    const uint64_t o_full = fast_total / F;
+    parts[0] = {0, o_full, F};
+    parts[1] = {o_full, o_full < count ? 1u : 0u, fast_total - o_full * F};
+    parts[2] = {o_full + 1, o_full + 1 < count ? count - o_full - 1 : 0, 0};
+  }
+  bool any = false;
+  for (const Part &pt : parts) any |= pt.cnt > 0 && need > pt.t_begin;
+  if (any) {
     GenericRestoreArgs ga{};
     // Temporaries for parameters that do not fit in the kernel arguments;
     // freed after a stream sync (only reached for k > 32 or k > 64 chunks).
     void *tmp_table = nullptr, *tmp_matrix = nullptr;
     hipError_t e = hipSuccess;
-    if (layout.pitch) {
-      ga.chunk_base = layout.base;
-      ga.chunk_pitch = layout.pitch;
-    } else if (k <= (uint32_t)kInlineChunks) {
-      for (uint32_t j = 0; j < k; ++j) ga.chunk_ptr[j] = chunks[j];
-    } else {
+    if (!layout.pitch && k > (uint32_t)kInlineChunks) {
       e = hipMalloc(&tmp_table, sizeof(uint8_t *) * k);
       if (e == hipSuccess) e = hipMemcpy(tmp_table, chunks, sizeof(uint8_t *) * k, hipMemcpyHostToDevice);
       ga.chunk_table = static_cast<const uint8_t *const *>(tmp_table);
@@ -323,15 +339,26 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_
         ga.matrix_dev = static_cast<const uint16_t *>(tmp_matrix);
       }
     }
-    if (e == hipSuccess) {
+    for (const Part &pt : parts) {
+      if (e != hipSuccess || pt.cnt == 0 || need <= pt.t_begin) continue;
+      if (tmp_table && pt.o0) {  // (k > 64: only reached without the fast path, i.e. o0 == 0)
+        e = hipErrorInvalidValue;
+        break;
+      }
+      if (layout.pitch) {
+        ga.chunk_base = layout.base + pt.o0 * chunk_stride;
+        ga.chunk_pitch = layout.pitch;
+      } else if (!tmp_table) {
+        for (uint32_t j = 0; j < k; ++j) ga.chunk_ptr[j] = chunks[j] + pt.o0 * chunk_stride;
+      }
       ga.chunk_stride = chunk_stride;
-      ga.count = count;
+      ga.count = (uint32_t)pt.cnt;
       ga.k = k;
       ga.cell_bytes = cb;
       ga.flags = flags;
-      ga.t_begin = fast_stripes;
-      ga.t_count = need - fast_stripes;
-      ga.out = out;
+      ga.t_begin = pt.t_begin;
+      ga.t_count = need - pt.t_begin;
+      ga.out = out + pt.o0 * out_stride;
       ga.out_stride = out_stride;
       ga.out_len = out_len;
       e = launch_restore_generic(ga, s);

@@ -164,6 +164,14 @@ int vds_ec_sha256_device(const uint8_t *base, uint64_t len, uint64_t stride, uin
 int vds_ec_encode16_hash_host(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data, uint64_t size,
                               uint8_t *const *outs, uint8_t *digests, unsigned flags);
 
+/* Content-addressed storage path of a replica from its SHA-256 name (host,
+ * no GPU): base64 (standard alphabet, '=' padding, encoding.cpp:136-174) with
+ * '+' -> '#' and '/' -> '_', split as chars [0,10) "/" [10,20) "/" [20,44)
+ * (dht_network_client.cpp:483-505, :632-653).  out receives count
+ * NUL-terminated paths of VDS_EC_PATH_BYTES bytes each.                     */
+#define VDS_EC_PATH_BYTES 48
+int vds_ec_replica_paths(const uint8_t *digests, uint32_t count, char *out);
+
 /* ----------------------------------------------------------------- utilities */
 /* Fill `size` device bytes at dst with the splitmix64 stream of `seed`
  * (little-endian 8-byte words) -- the synthetic-object generator used by

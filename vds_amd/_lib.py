@@ -61,6 +61,7 @@ SIGNATURES = {
     "vds_ec_sha256_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
     "vds_ec_encode16_hash_host": (C.c_int, [C.c_uint16, u16p, C.c_uint32, C.c_void_p, C.c_uint64, vpp, C.c_void_p,
                                             C.c_uint]),
+    "vds_ec_replica_paths": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "vds_ec_fill_splitmix_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]),
     "vds_ec_encode16_path": (C.c_int, [C.c_uint16, u16p, C.c_uint32, C.c_uint64]),
     "vds_ec_restore16_path": (C.c_int, [C.c_uint16, u16p, C.c_uint64]),

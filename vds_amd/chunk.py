@@ -28,7 +28,7 @@ from ._lib import F_CELLS, F_NO_TRAILER, VdsEcError, check
 __all__ = [
     "ChunkGenerator", "ChunkRestore", "ChunkStorage", "chunk_cells", "replica_size",
     "encode_device", "restore_device", "fill_splitmix_device", "encode_host_batch", "regenerate_host",
-    "regenerate_device", "sha256_device", "encode_hash_host",
+    "regenerate_device", "sha256_device", "encode_hash_host", "replica_storage_paths",
     "VdsEcError", "multipliers", "inverse",
 ]
 
@@ -294,6 +294,17 @@ def encode_hash_host(k: int, replicas: Sequence[int], data, write_padding: bool 
     check(_lib.lib().vds_ec_encode16_hash_host(k, _idp(ids, 2), ids.size, buf.ctypes.data if buf.size else None,
                                                buf.size, ptrs, digests.ctypes.data, flags), "encode16_hash_host")
     return [o[:L] for o in outs], [bytes(d) for d in digests[: ids.size]]
+
+
+def replica_storage_paths(digests) -> list:
+    """Storage paths <b64[0:10]>/<b64[10:20]>/<b64[20:]> of replicas from their
+    SHA-256 names (dht_network_client.cpp:483-505; base64 with '+' -> '#',
+    '/' -> '_').  Host-only."""
+    d = np.ascontiguousarray(np.frombuffer(b"".join(bytes(x) for x in digests), dtype=np.uint8))
+    count = d.size // 32
+    out = np.zeros(48 * max(count, 1), dtype=np.uint8)
+    check(_lib.lib().vds_ec_replica_paths(d.ctypes.data if count else None, count, out.ctypes.data), "replica_paths")
+    return [bytes(out[48 * i:48 * i + 46]).decode() for i in range(count)]
 
 
 def fill_splitmix_device(dst, size: int, seed: int, stream=None) -> None:

@@ -1037,6 +1037,34 @@ int vds_ec_encode16_hash_host(uint16_t k, const uint16_t *replicas, uint32_t n, 
   return hip_status(hipStreamSynchronize(c.stream));
 }
 
+int vds_ec_replica_paths(const uint8_t *digests, uint32_t count, char *out) {
+  if (count && (!digests || !out)) return VDS_EC_EINVAL;
+  static const char kB64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789#_";  // '+' '/' replaced
+  for (uint32_t i = 0; i < count; ++i) {
+    const uint8_t *d = digests + 32ull * i;
+    char b64[45];
+    int n = 0;
+    for (int p = 0; p + 2 < 32; p += 3) {  // 10 full groups
+      const uint32_t t = (uint32_t(d[p]) << 16) | (uint32_t(d[p + 1]) << 8) | d[p + 2];
+      for (int s = 18; s >= 0; s -= 6) b64[n++] = kB64[(t >> s) & 63];
+    }
+    const uint32_t t = (uint32_t(d[30]) << 16) | (uint32_t(d[31]) << 8);  // 2 bytes left: 3 chars + '='
+    b64[n++] = kB64[(t >> 18) & 63];
+    b64[n++] = kB64[(t >> 12) & 63];
+    b64[n++] = kB64[(t >> 6) & 63];
+    b64[n++] = '=';
+    char *o = out + (size_t)VDS_EC_PATH_BYTES * i;
+    std::memcpy(o, b64, 10);
+    o[10] = '/';
+    std::memcpy(o + 11, b64 + 10, 10);
+    o[21] = '/';
+    std::memcpy(o + 22, b64 + 20, 24);
+    o[46] = 0;
+    o[47] = 0;
+  }
+  return VDS_EC_OK;
+}
+
 int vds_ec_regenerate16_device(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
                                uint64_t chunk_stride, uint32_t count, const uint16_t *targets, uint32_t ntargets,
                                uint8_t *const *outs, uint64_t out_stride, void *stream) {

@@ -722,6 +722,10 @@ __device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t 
   }
 }
 
+#ifndef VDS_SYN_REC  // 2: scatter recovery with LDS XOR atomics; 1: gather (parks the syndromes)
+#define VDS_SYN_REC 2
+#endif
+
 #ifndef VDS_SYN_GM  // 1: interpolation by one additive-FFT level + half-size programs; 0: one 16-point program
 #define VDS_SYN_GM 1
 #endif
@@ -871,6 +875,53 @@ void k_restore_syn(SynRestoreArgs a) {
       }
     }
     __syncthreads();
+#if VDS_SYN_REC == 2
+    // ---- 2+3. wave j holds syndrome S_j whole and scatters its share of every
+    // recovered point, c_e[m] += R[m][j] S_j, into the erased slots (zero since
+    // stage 1) with LDS XOR atomics: T = x^b S_j walks the coefficient bits
+    // once for all M products, and no wave has to gather the syndromes (two
+    // barriers and a park/reload of the syndromes fewer than VDS_SYN_REC 1)
+    {
+      static_assert(S::kSynRows == 16 && S::kM == WV, "scatter recovery needs one whole syndrome per wave");
+      Plane16 t;
+#if VDS_DIAG_RES == 3
+      for (int r = 0; r < 16; ++r) t.p[r] = lane + r;
+#else
+      P::syndrome(kSynSameCode ? 1 : wave, L, t.p);
+#endif
+      if (tile + gridDim.x < a.total_tiles) load(tile + gridDim.x);
+      Plane16 ce[S::kM];
+#pragma unroll
+      for (int m = 0; m < S::kM; ++m) ce[m] = plane_zero();
+#pragma unroll
+      for (int b = 0; b < 16; b += 2) {
+        const Plane16 t1 = plane_mulx(t);
+#pragma unroll
+        for (int m = 0; m < S::kM; ++m) {
+          const uint32_t two = (a.solve_sel[m][b >> 2] >> (8 * (b & 3) + wave)) & 0x101u;
+          if (two == 1u)
+            ce[m] = plane_xor(ce[m], t);
+          else if (two == 0x100u)
+            ce[m] = plane_xor(ce[m], t1);
+          else if (two == 0x101u)
+            ce[m] = plane_xor3(ce[m], t, t1);
+        }
+        if (b < 14) t = plane_mulx(t1);
+      }
+      __syncthreads();  // every wave is done reading the zeroed erased planes
+#pragma unroll
+      for (int m = 0; m < S::kM; ++m) {
+        __attribute__((address_space(3))) uint64_t *dst =
+            (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * a.erased[m]);
+#pragma unroll
+        for (int h = 0; h < 8; ++h)
+          __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1),
+                                 (uint64_t)ce[m].p[2 * h] | ((uint64_t)ce[m].p[2 * h + 1] << 32), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    __syncthreads();
+#else
     // ---- 2. syndrome bit-rows of this wave, parked in the erased slots
     {
       uint32_t syn[S::kSynRows];
@@ -917,6 +968,7 @@ void k_restore_syn(SynRestoreArgs a) {
       __syncthreads();
     }
     __syncthreads();
+#endif
     if constexpr (REGEN) {
       // ---- 4'. regenerate: the recovered point e_w IS replica e_w's cells
       // (P(e_w) stripe by stripe).  Undo the stage-1 transpose and store it as

@@ -689,6 +689,44 @@ typedef __attribute__((address_space(3))) char lds_char;
 #endif
 constexpr bool kSynSameCode = VDS_SYN_SAME_CODE;
 
+// Diagnostic build (VDS_DIAG_STAMPS=1, timing only): every wave of
+// k_restore_syn accumulates s_memtime deltas per phase of its tiles into
+// g_syn_stamps[block][wave][phase] (read with vds_ec_diag_stamps; phases in
+// tools/syn_stamps.py).  The marks wait for outstanding scalar and LDS
+// operations and the compiler may move VALU work across them: read the
+// barrier waits, not the exact split of neighbouring phases.  Off: the marks
+// compile to nothing.
+#ifndef VDS_DIAG_STAMPS
+#define VDS_DIAG_STAMPS 0
+#endif
+constexpr int kStampPhases = 20;
+#if VDS_DIAG_STAMPS
+constexpr int kStampSlots = 4096 * 4 * kStampPhases;
+__device__ unsigned long long g_syn_stamps[kStampSlots];
+struct Stamps {
+  uint64_t prev, acc[kStampPhases];
+  __device__ __forceinline__ void init() {
+    prev = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < kStampPhases; ++i) acc[i] = 0;
+  }
+  __device__ __forceinline__ void mark(int i) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    acc[i] += now - prev;
+    prev = now;
+  }
+  __device__ __forceinline__ void flush(int slot, int lane) {
+    if (lane == 0 && slot < 4096 * 4)
+      for (int i = 0; i < kStampPhases; ++i) g_syn_stamps[slot * kStampPhases + i] = acc[i];
+  }
+};
+#else
+struct Stamps {
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void flush(int, int) {}
+};
+#endif
+
 // Group g of the plane-major LDS as seen by one lane.  ds_read_b128 carries a
 // 16-bit immediate offset, so groups past 64 KiB (points >= 16) are addressed
 // from a second base register; the base is laundered through an empty asm so
@@ -784,19 +822,23 @@ __device__ __forceinline__ void syn_gm_stage_c(const SynLds &L, uint32_t (&cells
 }
 
 template <int K, int N, int WV, int W>
-__device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)]) {
+__device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
   static_assert(K == 16 && (WV == 4 || WV == 8), "the one-level interpolation is laid out for k = 16");
   using P = RestorePrograms<K, N, WV>;
   constexpr int kPairs = (K / 2) / WV;           // stage-A pairs per wave
   constexpr int kHalfCells = P::kHalfRows / 16;  // stage-B cells per wave
   constexpr int kParts = WV / 2;                 // waves per half-size polynomial
   if constexpr (W < WV) {
-    if (wave != W) return syn_interp_gm<K, N, WV, W + 1>(wave, L, cells);
+    if (wave != W) return syn_interp_gm<K, N, WV, W + 1>(wave, L, cells, st);
     syn_gm_stage_a<W, kPairs>(L);
+    st.mark(7);
     __syncthreads();
+    st.mark(8);
     uint32_t half[P::kHalfRows];
     P::interpB(W, L, half);
+    st.mark(9);
     __syncthreads();  // every wave has read its Q values
+    st.mark(10);
     // P0 (W < kParts) or P1 cells kHalfCells (W % kParts) + c -> slot (K/2) (W / kParts) + ..
 #pragma unroll
     for (int c = 0; c < kHalfCells; ++c) {
@@ -805,8 +847,11 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
       for (int b = 0; b < 16; ++b) v[b] = half[16 * c + b];
       syn_put_point(L, (K / 2) * (W / kParts) + kHalfCells * (W % kParts) + c, v);
     }
+    st.mark(11);
     __syncthreads();
+    st.mark(12);
     syn_gm_stage_c<K, W, K / WV>(L, cells);
+    st.mark(13);
   }
 }
 
@@ -849,6 +894,8 @@ void k_restore_syn(SynRestoreArgs a) {
       for (int q = 0; q < 4; ++q) Q[s][q] = *reinterpret_cast<const u32x4 *>(src + 1024 * q);
     }
   };
+  Stamps st;
+  st.init();
   if (blockIdx.x < a.total_tiles) load(blockIdx.x);
   for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
     const uint32_t o = tile / a.tiles_per_obj;
@@ -874,7 +921,9 @@ void k_restore_syn(SynRestoreArgs a) {
         syn_put_point(L, a.point[wave * S::kLoadPer + s], Pl);
       }
     }
+    st.mark(0);
     __syncthreads();
+    st.mark(1);
 #if VDS_SYN_REC == 2
     // ---- 2+3. wave j holds syndrome S_j whole and scatters its share of every
     // recovered point, c_e[m] += R[m][j] S_j, into the erased slots (zero since
@@ -890,6 +939,7 @@ void k_restore_syn(SynRestoreArgs a) {
       P::syndrome(kSynSameCode ? 1 : wave, L, t.p);
 #endif
       if (tile + gridDim.x < a.total_tiles) load(tile + gridDim.x);
+      st.mark(2);
       Plane16 ce[S::kM];
 #pragma unroll
       for (int m = 0; m < S::kM; ++m) ce[m] = plane_zero();
@@ -908,7 +958,9 @@ void k_restore_syn(SynRestoreArgs a) {
         }
         if (b < 14) t = plane_mulx(t1);
       }
+      st.mark(3);
       __syncthreads();  // every wave is done reading the zeroed erased planes
+      st.mark(4);
 #pragma unroll
       for (int m = 0; m < S::kM; ++m) {
         __attribute__((address_space(3))) uint64_t *dst =
@@ -920,7 +972,9 @@ void k_restore_syn(SynRestoreArgs a) {
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
+    st.mark(5);
     __syncthreads();
+    st.mark(6);
 #else
     // ---- 2. syndrome bit-rows of this wave, parked in the erased slots
     {
@@ -994,7 +1048,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #if VDS_DIAG_RES == 1
       for (int r = 0; r < 16 * S::kCells; ++r) cells[r] = lane * r;
 #elif VDS_SYN_GM
-      syn_interp_gm<K, N, WV, 0>(wave, L, cells);
+      syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
 #else
       P::interp(kSynSameCode ? 1 : wave, L, cells);
 #endif
@@ -1009,6 +1063,7 @@ void k_restore_syn(SynRestoreArgs a) {
         // word group at a time keeps 32, not 64, transposed rows live.
         static_assert(2048 * 32 + 128 * 16 <= S::kLdsBytes, "staging layout is for 32-byte stripes");
         __syncthreads();
+        st.mark(14);
 #pragma unroll
         for (int g = 0; g < kGroups; ++g) {
           uint32_t rows[32];
@@ -1027,7 +1082,9 @@ void k_restore_syn(SynRestoreArgs a) {
                 rows[pi];
           }
         }
+        st.mark(15);
         __syncthreads();
+        st.mark(16);
         // 16-byte chunk c = 64 (kChunks wave + i) + lane of the tile: stripe c/2, half c%2
         constexpr int kChunks = 64 / WV;  // 1 KiB pieces of the tile each wave writes
         const lds_char *r0 =
@@ -1041,6 +1098,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #endif
           *reinterpret_cast<u32x4 *>(g0 + 1024 * i) = v;
         }
+        st.mark(17);
       } else {
         uint32_t rows[1][32];
 #pragma unroll
@@ -1061,8 +1119,17 @@ void k_restore_syn(SynRestoreArgs a) {
       }
     }
     __syncthreads();
+    st.mark(18);
   }
+  st.flush(blockIdx.x * WV + wave, lane);
 }
+
+#if VDS_DIAG_STAMPS
+extern "C" int vds_ec_diag_stamps(unsigned long long *host, size_t n) {
+  if (n > (size_t)kStampSlots) n = kStampSlots;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_syn_stamps), n * sizeof(unsigned long long));
+}
+#endif
 
 // ========================================================= generic regenerate
 

@@ -262,20 +262,24 @@ def _path(k, nodes, L):
     return _lib.lib().vds_ec_restore16_path(k, arr.ctypes.data_as(_lib.u16p), L)
 
 
-def test_syndrome_restore_erasure_patterns(ec):
-    """k_restore_syn<16,20>: any 16 of the 20 replicas, in any order."""
+@pytest.mark.parametrize("k,n", [(16, 20), (32, 40)])
+def test_syndrome_restore_erasure_patterns(ec, k, n):
+    """k_restore_syn<16,20> / <32,40>: any k of the n replicas, in any order."""
     import itertools
     import torch
     from vds_amd import chunk
-    k, n = 16, 20
+    m = n - k
     size = 2 * 2048 * 2 * k + 2 * k * 5 + 3  # two full tiles + generic tail
-    t = dev_object(torch, size, 2100)
+    t = dev_object(torch, size, 2100 + k)
     enc = dev_encode(torch, k, n, t, size)
     L = enc.shape[2]
     rng = np.random.default_rng(21)
-    combos = list(itertools.combinations(range(n), n - k))
-    picks = [combos[0], combos[-1], (0, 5, 10, 15), (16, 17, 18, 19)]
-    picks += [combos[i] for i in rng.choice(len(combos), 300, replace=False)]
+    picks = [tuple(range(m)), tuple(range(k, n)), tuple(range(0, n, n // m))[:m], tuple(range(k - m // 2, k + m // 2))]
+    if k == 16:
+        combos = list(itertools.combinations(range(n), m))
+        picks += [combos[i] for i in rng.choice(len(combos), 300, replace=False)]
+    else:  # C(40, 8) patterns: a random sample
+        picks += [tuple(sorted(int(x) for x in rng.choice(n, m, replace=False))) for _ in range(120)]
     out = torch.zeros(size + 64, dtype=torch.uint8, device="cuda")
     for erased in picks:
         nodes = [r for r in range(n) if r not in erased]
@@ -288,14 +292,14 @@ def test_syndrome_restore_erasure_patterns(ec):
         assert int(out[size:].sum().item()) == 0
 
 
-def test_syndrome_restore_arbitrary_chunks_vs_oracle(ec):
+@pytest.mark.parametrize("k,n", [(16, 20), (32, 40)])
+def test_syndrome_restore_arbitrary_chunks_vs_oracle(ec, k, n):
     """Chunks that are NOT codewords: the result must still be V_S^{-1} applied
     to the survivors, exactly as the reference's chunk_restore computes it."""
     import torch
     from vds_amd import chunk
-    k, n = 16, 20
-    rng = np.random.default_rng(22)
-    for trial in range(6):
+    rng = np.random.default_rng(22 + k)
+    for trial in range(6 if k == 16 else 3):
         tiles = int(rng.integers(1, 4))
         size = tiles * 2048 * 2 * k + int(rng.integers(0, 2 * k * 7))
         L = chunk.replica_size(k, size)

@@ -18,7 +18,7 @@
 // vds_amd/csrc/generated/restore_K_N.inc.  Points are processed in blocks so
 // the live temps of one block fit the register file.
 //
-//   gen_restore K N WAVES syndrome_block interp_block [half_block] > restore_K_N_wW.inc
+//   gen_restore K N WAVES syndrome_block interp_block [half_block [half_split]] > restore_K_N_wW.inc
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -184,8 +184,9 @@ static std::vector<std::vector<int>> all_bitrows(const std::vector<uint32_t> &M,
 // One wave's program: bit-rows [row0, row0 + nrows) of the map, points
 // blocked by `pb`.  The LDS reads of block b + 1 are issued before the XORs of
 // block b so their latency hides under them.
-static size_t emit_program(const char *name, const std::vector<std::vector<int>> &rows, int C, int row0, int nrows,
-                           int pb) {
+static size_t emit_program(const char *name, const std::vector<std::vector<int>> &rows, int C,
+                           const std::vector<int> &rowsel, int pb) {
+  const int nrows = (int)rowsel.size();
   std::printf("  template <typename In>\n  __device__ __forceinline__ static void %s(const In &IN4, uint32_t (&acc)[%d]) {\n",
               name, nrows);
   std::vector<Block> blocks;
@@ -193,7 +194,7 @@ static size_t emit_program(const char *name, const std::vector<std::vector<int>>
     const int cb = std::min(pb, C - c0);
     std::vector<std::vector<int>> sub(nrows);
     for (int r = 0; r < nrows; ++r)
-      for (int x : rows[row0 + r])
+      for (int x : rows[rowsel[r]])
         if (x >= 16 * c0 && x < 16 * (c0 + cb)) sub[r].push_back(x - 16 * c0);
     blocks.push_back(make_block(xorgen::paar(16 * cb, sub), c0));
   }
@@ -211,9 +212,15 @@ static size_t emit_program(const char *name, const std::vector<std::vector<int>>
   return ops;
 }
 
+static std::vector<int> row_range(int row0, int n) {
+  std::vector<int> v(n);
+  for (int i = 0; i < n; ++i) v[i] = row0 + i;
+  return v;
+}
+
 int main(int argc, char **argv) {
-  if (argc != 6 && argc != 7) {
-    std::fprintf(stderr, "usage: %s K N WAVES syndrome_block interp_block [half_interp_block]\n", argv[0]);
+  if (argc < 6 || argc > 8) {
+    std::fprintf(stderr, "usage: %s K N WAVES syndrome_block interp_block [half_interp_block [half_split]]\n", argv[0]);
     return 2;
   }
   const int K = std::atoi(argv[1]), N = std::atoi(argv[2]), M = N - K, waves = std::atoi(argv[3]);
@@ -259,12 +266,14 @@ int main(int argc, char **argv) {
   for (int w = 0; w < waves; ++w) {
     char name[64];
     std::snprintf(name, sizeof name, "syndrome%d", w);
-    total += emit_program(name, wrows, N, syn_rows * w, syn_rows, syn_pb);
+    total += emit_program(name, wrows, N, row_range(syn_rows * w, syn_rows), syn_pb);
   }
-  for (int w = 0; w < waves; ++w) {
+  // interp_block 0: no direct K-point programs (the kernel uses the
+  // additive-FFT stage B only; the direct ones are large for K = 32)
+  for (int w = 0; w < waves && int_pb > 0; ++w) {
     char name[64];
     std::snprintf(name, sizeof name, "interp%d", w);
-    total += emit_program(name, vrows, K, int_rows * w, int_rows, int_pb);
+    total += emit_program(name, vrows, K, row_range(int_rows * w, int_rows), int_pb);
   }
   // Half-size interpolation for the one-level additive-FFT interpolation
   // (k_restore_syn stage B): with G = {0, 2, .., K-2} and s(g) = g^2 + g,
@@ -277,12 +286,33 @@ int main(int argc, char **argv) {
   if (vds_ec_inverse16(H, dpts.data(), dinv.data()) != VDS_EC_OK) return 1;
   std::vector<uint32_t> Di(dinv.begin(), dinv.end());
   const auto drows = all_bitrows(Di, H, H);
+  // Cells (coefficients) of P0 / P1 per part: argv[7] gives the part of each
+  // of the H cells (default: contiguous), chosen to balance the programs.
+  std::vector<std::vector<int>> part_cells(hb_parts);
+  for (int c = 0; c < H; ++c) {
+    const int part = argc > 7 ? argv[7][c] - '0' : c / (H / hb_parts);
+    if (part < 0 || part >= hb_parts) return 1;
+    part_cells[part].push_back(c);
+  }
+  for (const auto &pc : part_cells)
+    if ((int)pc.size() != H / hb_parts) return 1;
   std::printf("  static constexpr int kHalfRows = %d;  // stage-B bit-rows per wave\n", hb_rows);
+  std::printf("  // stage-B cell c of part p (wave w: part w %% %d of P0 (w < %d) or P1)\n", hb_parts, hb_parts);
+  std::printf("  static constexpr uint8_t kHalfCell[%d][%d] = {", hb_parts, H / hb_parts);
+  for (int q = 0; q < hb_parts; ++q) {
+    std::printf("{");
+    for (int c : part_cells[q]) std::printf("%d, ", c);
+    std::printf("}, ");
+  }
+  std::printf("};\n");
   for (int w = 0; w < waves; ++w) {
     char name[64];
     std::snprintf(name, sizeof name, "interpB%d", w);
     g_par = w / hb_parts;
-    total_b += emit_program(name, drows, H, hb_rows * (w % hb_parts), hb_rows, hb_pb);
+    std::vector<int> rowsel;
+    for (int c : part_cells[w % hb_parts])
+      for (int b = 0; b < 16; ++b) rowsel.push_back(16 * c + b);
+    total_b += emit_program(name, drows, H, rowsel, hb_pb);
   }
   g_par = -1;
   std::printf("  template <typename In>\n  __device__ __forceinline__ static void interpB(int w, const In &IN4, uint32_t (&acc)[%d]) {\n", hb_rows);
@@ -290,6 +320,7 @@ int main(int argc, char **argv) {
   for (int w = 0; w < waves; ++w) std::printf("      case %d: interpB%d(IN4, acc); break;\n", w, w);
   std::printf("      default: break;\n    }\n  }\n");
   for (const char *kind : {"syndrome", "interp"}) {
+    if (kind[0] == 'i' && int_pb == 0) continue;
     std::printf("  template <typename In>\n  __device__ __forceinline__ static void %s(int w, const In &IN4, uint32_t (&acc)[%d]) {\n",
                 kind, kind[0] == 's' ? syn_rows : int_rows);
     std::printf("    switch (w) {\n");

@@ -653,6 +653,7 @@ template <int K, int N, int WV> struct RestorePrograms;
 #include "generated/restore_16_20_w4.inc"
 #endif
 #endif
+#include "generated/restore_32_40_w8.inc"
 #undef VDS_SCHED_FENCE
 
 // k_restore_syn<K, N, WV>: one 2048-stripe tile per workgroup of WV waves.
@@ -733,11 +734,13 @@ struct Stamps {
 // the compiler does not fold it back into one address register per group.
 struct SynLds {
   lds_char *base;
-  uint32_t lo;  // 16 * lane
-  uint32_t hi;  // 16 * lane + 64 KiB (opaque)
+  uint32_t lo;   // 16 * lane
+  uint32_t hi;   // 16 * lane + 64 KiB (opaque)
+  uint32_t hi2;  // 16 * lane + 128 KiB (opaque; points 32.. of k = 32)
   __device__ __forceinline__ u32x4 operator()(int g) const {
     if (g < 64) return *(lds_v4 *)(base + lo + g * 1024);
-    return *(lds_v4 *)(base + hi + (g - 64) * 1024);
+    if (g < 128) return *(lds_v4 *)(base + hi + (g - 64) * 1024);
+    return *(lds_v4 *)(base + hi2 + (g - 128) * 1024);
   }
   __device__ __forceinline__ void put(int g, u32x4 v) const {
     *(lds_v4 *)(base + lo + g * 1024) = v;  // runtime g: one address add
@@ -823,7 +826,8 @@ __device__ __forceinline__ void syn_gm_stage_c(const SynLds &L, uint32_t (&cells
 
 template <int K, int N, int WV, int W>
 __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
-  static_assert(K == 16 && (WV == 4 || WV == 8), "the one-level interpolation is laid out for k = 16");
+  static_assert((K == 16 && (WV == 4 || WV == 8)) || (K == 32 && WV == 8),
+                "the one-level interpolation is laid out for k = 16 and k = 32");
   using P = RestorePrograms<K, N, WV>;
   constexpr int kPairs = (K / 2) / WV;           // stage-A pairs per wave
   constexpr int kHalfCells = P::kHalfRows / 16;  // stage-B cells per wave
@@ -879,6 +883,12 @@ void k_restore_syn(SynRestoreArgs a) {
   L.lo = 16u * lane;
   L.hi = 16u * lane + 65536u;
   asm volatile("" : "+v"(L.hi));
+  if constexpr (N * 16 > 128) {
+    L.hi2 = 16u * lane + 131072u;
+    asm volatile("" : "+v"(L.hi2));
+  } else {
+    L.hi2 = L.hi;
+  }
   const int my_erased = wave < S::kM ? a.erased[wave] : 0;
 
   // survivor staging: the next tile's loads are issued after the syndrome
@@ -896,6 +906,11 @@ void k_restore_syn(SynRestoreArgs a) {
   };
   Stamps st;
   st.init();
+  // k = 32 (one 160 KiB workgroup per CU): the prefetched survivors would be
+  // live across the syndrome and stage-B programs, which then spill; they are
+  // issued after the interpolation instead and land under the staging and
+  // stores (REGEN has no interpolation and keeps the early issue)
+  constexpr bool kLateLoad = K == 32 && !REGEN && VDS_SYN_GM;
   if (blockIdx.x < a.total_tiles) load(blockIdx.x);
   for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
     const uint32_t o = tile / a.tiles_per_obj;
@@ -938,38 +953,48 @@ void k_restore_syn(SynRestoreArgs a) {
 #else
       P::syndrome(kSynSameCode ? 1 : wave, L, t.p);
 #endif
-      if (tile + gridDim.x < a.total_tiles) load(tile + gridDim.x);
+      if (!kLateLoad && tile + gridDim.x < a.total_tiles) load(tile + gridDim.x);
       st.mark(2);
-      Plane16 ce[S::kM];
+      // M <= 4: all products before the barrier (their walk overlaps the
+      // slower waves' syndromes); M = 8: four at a time after it (eight
+      // accumulators would not fit beside the prefetched survivors)
+      constexpr int kMC = S::kM <= 4 ? S::kM : 4;
+      if constexpr (kMC < S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
 #pragma unroll
-      for (int m = 0; m < S::kM; ++m) ce[m] = plane_zero();
+      for (int m0 = 0; m0 < S::kM; m0 += kMC) {
+        Plane16 ce[kMC];
 #pragma unroll
-      for (int b = 0; b < 16; b += 2) {
-        const Plane16 t1 = plane_mulx(t);
+        for (int m = 0; m < kMC; ++m) ce[m] = plane_zero();
+        Plane16 t_copy;  // several chunks walk from the same syndrome
+        Plane16 &tt = kMC < S::kM ? (t_copy = t, t_copy) : t;
 #pragma unroll
-        for (int m = 0; m < S::kM; ++m) {
-          const uint32_t two = (a.solve_sel[m][b >> 2] >> (8 * (b & 3) + wave)) & 0x101u;
-          if (two == 1u)
-            ce[m] = plane_xor(ce[m], t);
-          else if (two == 0x100u)
-            ce[m] = plane_xor(ce[m], t1);
-          else if (two == 0x101u)
-            ce[m] = plane_xor3(ce[m], t, t1);
+        for (int b = 0; b < 16; b += 2) {
+          const Plane16 t1 = plane_mulx(tt);
+#pragma unroll
+          for (int m = 0; m < kMC; ++m) {
+            const uint32_t two = (a.solve_sel[m0 + m][b >> 2] >> (8 * (b & 3) + wave)) & 0x101u;
+            if (two == 1u)
+              ce[m] = plane_xor(ce[m], tt);
+            else if (two == 0x100u)
+              ce[m] = plane_xor(ce[m], t1);
+            else if (two == 0x101u)
+              ce[m] = plane_xor3(ce[m], tt, t1);
+          }
+          if (b < 14) tt = plane_mulx(t1);
         }
-        if (b < 14) t = plane_mulx(t1);
-      }
-      st.mark(3);
-      __syncthreads();  // every wave is done reading the zeroed erased planes
-      st.mark(4);
+        st.mark(3);
+        if constexpr (kMC == S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
+        st.mark(4);
 #pragma unroll
-      for (int m = 0; m < S::kM; ++m) {
-        __attribute__((address_space(3))) uint64_t *dst =
-            (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * a.erased[m]);
+        for (int m = 0; m < kMC; ++m) {
+          __attribute__((address_space(3))) uint64_t *dst =
+              (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * a.erased[m0 + m]);
 #pragma unroll
-        for (int h = 0; h < 8; ++h)
-          __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1),
-                                 (uint64_t)ce[m].p[2 * h] | ((uint64_t)ce[m].p[2 * h + 1] << 32), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          for (int h = 0; h < 8; ++h)
+            __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1),
+                                   (uint64_t)ce[m].p[2 * h] | ((uint64_t)ce[m].p[2 * h + 1] << 32), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
     }
     st.mark(5);
@@ -1049,6 +1074,7 @@ void k_restore_syn(SynRestoreArgs a) {
       for (int r = 0; r < 16 * S::kCells; ++r) cells[r] = lane * r;
 #elif VDS_SYN_GM
       syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
+      if (kLateLoad && tile + gridDim.x < a.total_tiles) load(tile + gridDim.x);
 #else
       P::interp(kSynSameCode ? 1 : wave, L, cells);
 #endif
@@ -1097,6 +1123,50 @@ void k_restore_syn(SynRestoreArgs a) {
           if (a.out_stride == 1)
 #endif
           *reinterpret_cast<u32x4 *>(g0 + 1024 * i) = v;
+        }
+        st.mark(17);
+      } else if constexpr (K == 32) {
+        // Stage as for k = 16 with 64-byte stripes and 8 bytes of padding
+        // after every 8 stripes: stripe st, word w at st*64 + (st/8)*8 + 4w;
+        // the copy-out reads 16 bytes per lane as two 8-byte-aligned halves.
+        static_assert(S::kCells == 4 && 2048 * 64 + 256 * 8 <= S::kLdsBytes, "staging layout is for 64-byte stripes");
+        __syncthreads();
+        st.mark(14);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          uint32_t rows[32];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int jb = 0; jb < 16; ++jb) rows[16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
+          transpose32(rows, bm);
+          // slot 8q+e is stripe st = 8 lane + 512 q + e: byte 512 lane + 8 lane
+          // + q (32768 + 512) + 64 e + 4 (2 wave + g); lanes l and l + 16 of a
+          // 32-lane group share a bank (one word group at a time keeps 32,
+          // not 64, transposed rows live)
+          lds_char *w0 = L.base + 520u * lane + 4u * (2 * wave + g);
+#pragma unroll
+          for (int slot = 0; slot < 32; ++slot) {
+            const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+            *(__attribute__((address_space(3))) uint32_t *)(w0 + (slot >> 3) * (32768 + 512) + (slot & 7) * 64) =
+                rows[pi];
+          }
+        }
+        st.mark(15);
+        __syncthreads();
+        st.mark(16);
+        // 16-byte chunk c = 64 (16 wave + i) + lane of the tile: stripe c/4, quarter c%4
+        uint8_t *g0 = dst + stripe0 * (2 * K) + 16384u * wave + 16u * lane;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t c = 64u * (16u * wave + i) + lane;
+          const lds_char *r = L.base + 64u * (c >> 2) + 8u * (c >> 5) + 16u * (c & 3);
+          const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
+          const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
+#if VDS_DIAG_RES == 2
+          if (a.out_stride == 1)
+#endif
+          *reinterpret_cast<u32x4 *>(g0 + 1024 * i) = u32x4{v0[0], v0[1], v1[0], v1[1]};
         }
         st.mark(17);
       } else {
@@ -1290,12 +1360,13 @@ hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t
 }
 
 
-bool has_restore_syn(uint32_t k, uint32_t n) { return k == 16 && n == 20; }
+bool has_restore_syn(uint32_t k, uint32_t n) { return (k == 16 && n == 20) || (k == 32 && n == 40); }
 
 constexpr int kSynWaves16 = VDS_SYN_WAVES;
 
 const uint16_t *restore_syn_weights(uint32_t k, uint32_t n) {
   if (k == 16 && n == 20) return &RestorePrograms<16, 20, kSynWaves16>::kSyndromeW[0][0];
+  if (k == 32 && n == 40) return &RestorePrograms<32, 40, 8>::kSyndromeW[0][0];
   return nullptr;
 }
 
@@ -1321,6 +1392,8 @@ hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, h
   if (k == 16 && n == 20)
     return regen ? launch_restore_syn_kn<16, 20, kSynWaves16, true>(a, s)
                  : launch_restore_syn_kn<16, 20, kSynWaves16, false>(a, s);
+  if (k == 32 && n == 40)
+    return regen ? launch_restore_syn_kn<32, 40, 8, true>(a, s) : launch_restore_syn_kn<32, 40, 8, false>(a, s);
   return hipErrorNotSupported;
 }
 

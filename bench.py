@@ -89,16 +89,17 @@ def kernel_names(k, n, nodes, size, L):
     return enc, rep
 
 
-def pmc_traffic(path, kernel, objects):
+def pmc_traffic(path, kernel, objects, k, n):
     """roofline.traffic: HBM bytes per launch of `kernel` from the committed
-    rocprofv3 FETCH_SIZE/WRITE_SIZE passes (bytes per object x objects)."""
+    rocprofv3 FETCH_SIZE/WRITE_SIZE passes (bytes per object x objects), only
+    when they were measured on the same code shape (k, n)."""
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None, None
     e = t.get(kernel.split("<")[0])
-    if not e:
+    if not e or (e.get("k", 16), e.get("n", 20)) != (k, n):
         return None, None
     return round(e["bytes_per_object"] * objects), f"{os.path.relpath(path, ROOT)}: {e['source']}"
 
@@ -254,7 +255,7 @@ def main():
     else:
         dom, dom_bytes, dom_ms = rep_name, rep_bytes, rep_ms
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.traffic_json, dom, objects)
+    traffic, traffic_src = pmc_traffic(args.traffic_json, dom, objects, k, n)
 
     result = {
         "metric": "device-resident encode+repair GiB/s, k=16 m=4 64 MiB stripes, 1/2/4/8 GPU",

@@ -34,11 +34,11 @@ def main():
     fetch = per_kernel(f"{fdir}/run_counter_collection.csv", "FETCH_SIZE")
     write = per_kernel(f"{wdir}/run_counter_collection.csv", "WRITE_SIZE")
     res = {}
-    for k in sorted(set(fetch) & set(write)):
-        if not k.startswith("k_") or k == "k_fill_splitmix":
+    for name in sorted(set(fetch) & set(write)):
+        if not name.startswith("k_") or name == "k_fill_splitmix":
             continue
-        f2, w = 2 * fetch[k], write[k]
-        res[k] = {"bytes_per_object": (f2 + w) / objects, "fetch_bytes_per_object": f2 / objects,
+        f2, w = 2 * fetch[name], write[name]
+        res[name] = {"bytes_per_object": (f2 + w) / objects, "fetch_bytes_per_object": f2 / objects,
                   "write_bytes_per_object": w / objects, "objects_per_launch": objects, "k": k, "n": n,
                   "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 streaming-read correction) and --pmc "
                             "WRITE_SIZE, separate passes, mean over launches"}

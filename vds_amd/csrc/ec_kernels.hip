@@ -737,14 +737,19 @@ struct SynLds {
   uint32_t lo;   // 16 * lane
   uint32_t hi;   // 16 * lane + 64 KiB (opaque)
   uint32_t hi2;  // 16 * lane + 128 KiB (opaque; points 32.. of k = 32)
-  __device__ __forceinline__ u32x4 operator()(int g) const {
-    if (g < 64) return *(lds_v4 *)(base + lo + g * 1024);
-    if (g < 128) return *(lds_v4 *)(base + hi + (g - 64) * 1024);
-    return *(lds_v4 *)(base + hi2 + (g - 128) * 1024);
+  // A compile-time group is an immediate offset (< 64 KiB) from one of the
+  // three bases, so no per-group address register stays live; a runtime
+  // group costs one address add.
+  __device__ __forceinline__ lds_char *at(int g) const {
+    if (__builtin_constant_p(g)) {
+      if (g < 64) return base + lo + g * 1024;
+      if (g < 128) return base + hi + (g - 64) * 1024;
+      return base + hi2 + (g - 128) * 1024;
+    }
+    return base + lo + g * 1024;
   }
-  __device__ __forceinline__ void put(int g, u32x4 v) const {
-    *(lds_v4 *)(base + lo + g * 1024) = v;  // runtime g: one address add
-  }
+  __device__ __forceinline__ u32x4 operator()(int g) const { return *(lds_v4 *)at(g); }
+  __device__ __forceinline__ void put(int g, u32x4 v) const { *(lds_v4 *)at(g) = v; }
 };
 
 __device__ __forceinline__ void syn_put_point(const SynLds &L, int pt, const uint32_t (&v)[16]) {
@@ -755,13 +760,17 @@ __device__ __forceinline__ void syn_put_point(const SynLds &L, int pt, const uin
 __device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t (&v)[16]) {
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    const u32x4 x = *(lds_v4 *)(L.base + L.lo + (4 * pt + g) * 1024);
+    const u32x4 x = L(4 * pt + g);
     v[4 * g] = x[0];
     v[4 * g + 1] = x[1];
     v[4 * g + 2] = x[2];
     v[4 * g + 3] = x[3];
   }
 }
+
+#ifndef VDS_SYN_LATE  // k = 32: 1 issues the next tile's survivor loads after the interpolation, 0 after the syndromes
+#define VDS_SYN_LATE 1
+#endif
 
 #ifndef VDS_SYN_REC  // 2: scatter recovery with LDS XOR atomics; 1: gather (parks the syndromes)
 #define VDS_SYN_REC 2
@@ -910,7 +919,7 @@ void k_restore_syn(SynRestoreArgs a) {
   // live across the syndrome and stage-B programs, which then spill; they are
   // issued after the interpolation instead and land under the staging and
   // stores (REGEN has no interpolation and keeps the early issue)
-  constexpr bool kLateLoad = K == 32 && !REGEN && VDS_SYN_GM;
+  constexpr bool kLateLoad = VDS_SYN_LATE && K == 32 && !REGEN && VDS_SYN_GM;
   if (blockIdx.x < a.total_tiles) load(blockIdx.x);
   for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
     const uint32_t o = tile / a.tiles_per_obj;
@@ -1155,12 +1164,14 @@ void k_restore_syn(SynRestoreArgs a) {
         st.mark(15);
         __syncthreads();
         st.mark(16);
-        // 16-byte chunk c = 64 (16 wave + i) + lane of the tile: stripe c/4, quarter c%4
+        // 16-byte chunk c = 64 (16 wave + i) + lane of the tile: stripe c/4,
+        // quarter c%4, at 64 (c/4) + 8 (c/32) + 16 (c%4) = r0 + 1040 i (one
+        // per-lane base, compile-time offsets: no hoisted address per i)
         uint8_t *g0 = dst + stripe0 * (2 * K) + 16384u * wave + 16u * lane;
+        const lds_char *r0 = L.base + 16640u * wave + 64u * (lane >> 2) + 8u * (lane >> 5) + 16u * (lane & 3);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const uint32_t c = 64u * (16u * wave + i) + lane;
-          const lds_char *r = L.base + 64u * (c >> 2) + 8u * (c >> 5) + 16u * (c & 3);
+          const lds_char *r = r0 + 1040 * i;
           const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
           const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
 #if VDS_DIAG_RES == 2

@@ -151,6 +151,16 @@ int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
                                const uint8_t *const *objs, const uint64_t *sizes, uint32_t count,
                                uint8_t *const *outs, unsigned flags, int max_devices);
 
+/* Batched host-memory restore across every visible GPU (the restore side of
+ * the batch above; chunk_storage::restore_data, chunk_storage.cpp:62-85, per
+ * object).  Object o is restored from the k host chunks chunks[o*k + j] of
+ * chunk_sizes[o] bytes holding replicas nodes[o*k + j]; on entry out_sizes[o]
+ * is the capacity of outs[o], on success the restored length (trailer-trimmed
+ * as vds_ec_restore16_host).  Every object is validated before any transfer. */
+int vds_ec_restore16_host_batch(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks,
+                                const uint64_t *chunk_sizes, uint32_t count, uint8_t *const *outs, uint64_t *out_sizes,
+                                unsigned flags, int max_devices);
+
 /* ---------------------------------------------------------- replica names
  * The reference names each replica by SHA-256 of its bytes (save_temp /
  * save_data: dht_network_client.cpp:79, :593 -> hash::signature(sha256),

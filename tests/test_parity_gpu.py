@@ -485,3 +485,33 @@ def test_host_batch_multi_device(ec):
     for o, d in zip(outs, objs):
         for r in (0, 3, 19):
             assert np.array_equal(o[r], O.encode(16, r, d))
+
+
+@pytest.mark.parametrize("k,n", [(16, 20), (32, 40), (4, 6)])
+def test_restore_host_batch(ec, k, n):
+    """vds_ec_restore16_host_batch: per-object survivor sets and sizes, bit-exact
+    against the oracle's restore (chunk.h:402-444) of the same chunks."""
+    from vds_amd._lib import VdsEcError
+    rng = np.random.default_rng(31 + k)
+    sizes = [1, 2 * k * 2048 * 2 + 7, 65536 * 3 + 1, 2 * k, 300001]
+    objs = [rng.integers(0, 256, s, dtype=np.uint8) for s in sizes]
+    nodes, chunks = [], []
+    for d in objs:
+        ids = [int(x) for x in rng.choice(n, k, replace=False)]
+        nodes.append(ids)
+        chunks.append([O.encode(k, r, d) for r in ids])
+    got = ec.restore_host_batch(k, nodes, chunks)
+    for d, g, ids, ch in zip(objs, got, nodes, chunks):
+        assert np.array_equal(g, d), (k, d.size, ids)
+        assert np.array_equal(g, O.restore(k, ids, ch))
+    # one id list for every object
+    ids = list(range(n - k, n))
+    same = ec.restore_host_batch(k, ids, [[O.encode(k, r, d) for r in ids] for d in objs[:3]])
+    assert all(np.array_equal(g, d) for g, d in zip(same, objs[:3]))
+    with pytest.raises(VdsEcError):  # chunks of one object differ in size (chunk_storage.cpp:73-76)
+        ec.restore_host_batch(k, [nodes[0]], [[c[:-1] if j == 0 else c for j, c in enumerate(chunks[1])]])
+    bad = [c.copy() for c in chunks[1]]
+    for c in bad:  # a trailer claiming more bytes than the chunks hold: the reference's fatal error
+        c[-2], c[-1] = 0xFF, 0xFF
+    with pytest.raises(VdsEcError):
+        ec.restore_host_batch(k, [nodes[1]], [bad])

@@ -7,10 +7,10 @@ this package is the Python host mirror of the reference's API.
 from ._lib import VdsEcError, device_count
 from .chunk import (ChunkGenerator, ChunkRestore, ChunkStorage, chunk_cells, encode_device,
                     encode_host_batch, fill_splitmix_device, inverse, multipliers, replica_size,
-                    restore_device)
+                    restore_device, restore_host_batch)
 
 __all__ = [
     "ChunkGenerator", "ChunkRestore", "ChunkStorage", "chunk_cells", "encode_device", "restore_device",
-    "fill_splitmix_device", "encode_host_batch", "inverse", "multipliers", "replica_size", "VdsEcError",
+    "fill_splitmix_device", "encode_host_batch", "restore_host_batch", "inverse", "multipliers", "replica_size", "VdsEcError",
     "device_count",
 ]

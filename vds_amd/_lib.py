@@ -54,6 +54,7 @@ SIGNATURES = {
     "vds_ec_restore8_host": (C.c_int, [C.c_uint8, u8p, vpp, C.c_uint64, C.c_void_p, u64p, C.c_uint]),
     "vds_ec_encode16_host_batch": (C.c_int, [C.c_uint16, u16p, C.c_uint32, vpp, u64p, C.c_uint32, vpp,
                                              C.c_uint, C.c_int]),
+    "vds_ec_restore16_host_batch": (C.c_int, [C.c_uint16, u16p, vpp, u64p, C.c_uint32, vpp, u64p, C.c_uint, C.c_int]),
     "vds_ec_regenerate16_device": (C.c_int, [C.c_uint16, u16p, vpp, C.c_uint64, C.c_uint64, C.c_uint32, u16p,
                                              C.c_uint32, vpp, C.c_uint64, C.c_void_p]),
     "vds_ec_regenerate16_host": (C.c_int, [C.c_uint16, u16p, vpp, C.c_uint64, u16p, C.c_uint32, vpp]),

@@ -27,7 +27,8 @@ from ._lib import F_CELLS, F_NO_TRAILER, VdsEcError, check
 
 __all__ = [
     "ChunkGenerator", "ChunkRestore", "ChunkStorage", "chunk_cells", "replica_size",
-    "encode_device", "restore_device", "fill_splitmix_device", "encode_host_batch", "regenerate_host",
+    "encode_device", "restore_device", "fill_splitmix_device", "encode_host_batch", "restore_host_batch",
+    "regenerate_host",
     "regenerate_device", "sha256_device", "encode_hash_host", "replica_storage_paths",
     "VdsEcError", "multipliers", "inverse",
 ]
@@ -310,6 +311,38 @@ def replica_storage_paths(digests) -> list:
 def fill_splitmix_device(dst, size: int, seed: int, stream=None) -> None:
     ptr = dst.data_ptr() if hasattr(dst, "data_ptr") else int(dst)
     check(_lib.lib().vds_ec_fill_splitmix_device(ptr, size, seed, _stream_ptr(stream)), "fill_splitmix")
+
+
+def restore_host_batch(k: int, nodes: Sequence, chunks: Sequence[Sequence], max_devices: int = 0,
+                       outs: list | None = None) -> list:
+    """Multi-GPU host-memory restore of many objects (chunk_storage::restore_data
+    per object, chunk_storage.cpp:62-85).  `chunks[o]` are the k replicas of
+    object o, holding replica ids `nodes[o]` (or one id list for every object).
+    `outs[o]` (optional) are caller-owned uint8 buffers; each must hold the
+    restored object.  Returns the restored objects (trailer-trimmed, as
+    restore16_host), as views of `outs` when given."""
+    count = len(chunks)
+    per = [list(nodes)] * count if count and np.ndim(nodes) == 1 else [list(n) for n in nodes]
+    if len(per) != count or any(len(n) != k or len(c) != k for n, c in zip(per, chunks)):
+        raise VdsEcError(_lib.EINVAL, "restore_host_batch: need k ids and k chunks per object")
+    bufs = [[_u8(c) for c in row] for row in chunks]
+    if any(c.size != row[0].size for row in bufs for c in row):  # chunk_storage.cpp:73-76
+        raise VdsEcError(_lib.EINVAL, "restore_host_batch: chunks of one object differ in size")
+    sizes = np.array([row[0].size for row in bufs], dtype=np.uint64)
+    ids = np.ascontiguousarray(np.array(per, dtype=np.uint16).reshape(-1))
+    if outs is None:
+        outs = [np.empty(max(int(s) * k, 1), dtype=np.uint8) for s in sizes]
+    outs = [_u8(o) for o in outs]
+    if len(outs) != count:
+        raise VdsEcError(_lib.EINVAL, "restore_host_batch: one output buffer per object")
+    caps = np.array([o.size for o in outs], dtype=np.uint64)
+    cptrs = (C.c_void_p * max(1, count * k))(*[c.ctypes.data for row in bufs for c in row])
+    optrs = (C.c_void_p * max(1, count))(*[o.ctypes.data for o in outs])
+    check(_lib.lib().vds_ec_restore16_host_batch(k, ids.ctypes.data_as(_lib.u16p), cptrs,
+                                                 sizes.ctypes.data_as(_lib.u64p), count, optrs,
+                                                 caps.ctypes.data_as(_lib.u64p), 0, max_devices),
+          "restore16_host_batch")
+    return [o[: int(n)] for o, n in zip(outs, caps)]
 
 
 def encode_host_batch(k: int, replicas: Sequence[int], objects: Sequence, max_devices: int = 0,

@@ -996,6 +996,94 @@ int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
   return status.load();
 }
 
+int vds_ec_restore16_host_batch(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks,
+                                const uint64_t *chunk_sizes, uint32_t count, uint8_t *const *outs, uint64_t *out_sizes,
+                                unsigned flags, int max_devices) {
+  if (k == 0 || (count && (!nodes || !chunks || !chunk_sizes || !outs || !out_sizes))) return VDS_EC_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VDS_EC_ENODEV;
+  if (max_devices > 0 && max_devices < ndev) ndev = max_devices;
+  if (count == 0) return VDS_EC_OK;
+  // Validate every object before any transfer, as restore16_host does per
+  // object (chunk.h:415-419 lengths; the trailer of the first chunk), so a
+  // bad object fails the call without partial output.
+  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
+  std::vector<uint64_t> lens(count);
+  for (uint32_t o = 0; o < count; ++o) {
+    const uint64_t cs = chunk_sizes[o];
+    int rc = check_restore_args(k, nodes + (uint64_t)o * k, chunks + (uint64_t)o * k, cs);
+    if (rc) return rc;
+    const uint8_t *c0 = chunks[(uint64_t)o * k];
+    const uint16_t padding = (cells || cs < 2) ? 0 : (uint16_t)((c0[cs - 2] << 8) | c0[cs - 1]);
+    bool ok = true;
+    lens[o] = restored_len(2, k, cs, padding, flags, &ok);
+    if (!ok) return VDS_EC_ERESTORE;
+    if (lens[o] > out_sizes[o] || (lens[o] && !outs[o])) return VDS_EC_EINVAL;
+  }
+  std::atomic<int> status{VDS_EC_OK};
+  auto worker = [&](int dev) {
+    if (hipSetDevice(dev) != hipSuccess) {
+      status = VDS_EC_ENODEV;
+      return;
+    }
+    // The encode batch's ring: while one slot's object is on the GPU, the
+    // other slot's pinned staging is filled with the next object's chunks or
+    // drained into the caller's buffer.
+    BatchRing *ring = batch_ring(dev);
+    if (!ring) {
+      status = VDS_EC_ENODEV;
+      return;
+    }
+    std::lock_guard<std::mutex> hold(ring->mu);
+    auto drain = [&](BatchSlot &s) -> int {
+      if (s.obj < 0) return VDS_EC_OK;
+      hipError_t e = hipStreamSynchronize(s.stream);
+      if (e != hipSuccess) return hip_status(e);
+      if (lens[s.obj]) parallel_copy({{outs[s.obj], s.h_out}}, lens[s.obj]);
+      s.obj = -1;
+      return VDS_EC_OK;
+    };
+    int si = 0;
+    for (int64_t o = dev; o < (int64_t)count && status.load() == VDS_EC_OK; o += ndev, si ^= 1) {
+      BatchSlot &s = ring->slot[si];
+      int rc = drain(s);
+      if (rc) { status = rc; break; }
+      const uint64_t cs = chunk_sizes[o];
+      const uint16_t *nd = nodes + (uint64_t)o * k;
+      std::vector<uint16_t> m((size_t)k * k);
+      rc = inverse16(k, nd, m.data());
+      if (rc) { status = rc; break; }
+      rc = s.reserve(cs * k ? cs * k : 1, lens[o] ? lens[o] : 1);
+      if (rc) { status = rc; break; }
+      std::vector<std::pair<uint8_t *, const uint8_t *>> parts(k);
+      for (uint32_t j = 0; j < k; ++j) parts[j] = {s.h_in + (uint64_t)j * cs, chunks[(uint64_t)o * k + j]};
+      if (cs) parallel_copy(parts, cs);
+      hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, cs * k, hipMemcpyHostToDevice, s.stream);
+      if (e != hipSuccess) { status = hip_status(e); break; }
+      std::vector<const uint8_t *> dchunks(k);
+      for (uint32_t j = 0; j < k; ++j) dchunks[j] = s.d_in + (uint64_t)j * cs;
+      rc = restore_device(2, k, nd, m.data(), dchunks.data(), cs, 0, lens[o], 1, s.d_out, 0, flags, s.stream);
+      if (rc) { status = rc; break; }
+      if (lens[o]) {
+        e = hipMemcpyAsync(s.h_out, s.d_out, lens[o], hipMemcpyDeviceToHost, s.stream);
+        if (e != hipSuccess) { status = hip_status(e); break; }
+      }
+      s.obj = o;
+    }
+    for (auto &s : ring->slot) {
+      int rc = drain(s);
+      if (rc && status.load() == VDS_EC_OK) status = rc;
+      s.obj = -1;
+    }
+  };
+  std::vector<std::thread> threads;
+  for (int d = 0; d < ndev; ++d) threads.emplace_back(worker, d);
+  for (auto &t : threads) t.join();
+  if (status.load() == VDS_EC_OK)
+    for (uint32_t o = 0; o < count; ++o) out_sizes[o] = lens[o];
+  return status.load();
+}
+
 int vds_ec_sha256_device(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count, uint8_t *digests,
                          void *stream) {
   if (count && (!digests || (len && !base))) return VDS_EC_EINVAL;

@@ -141,6 +141,18 @@ static void chunk_test_regenerate() {
     ASSERT_EQ(0, std::memcmp(again.data(), fused[i].data(), again.size()));
     ASSERT_EQ(0, std::memcmp(reps[lost[i]].data(), fused[i].data(), again.size()));
   }
+  // batched restore_data: the same objects as one call per object
+  std::vector<std::unordered_map<uint16_t, vds::const_data_buffer>> batch = {survivors, survivors};
+  batch[1].erase(1);
+  batch[1][0] = reps[0];
+  GET_EXPECTED_TEST(objects, storage.restore_datas(batch));
+  ASSERT_EQ(size_t(2), objects.size());
+  for (auto &o : objects) {
+    ASSERT_EQ(object.size(), o.size());
+    ASSERT_EQ(0, std::memcmp(object.data(), o.data(), o.size()));
+  }
+  batch[0].erase(2);  // k - 1 horcruxes: restore_data's error
+  ASSERT_EQ(false, storage.restore_datas(batch).has_value());
   // names: the replica hash is a function of the bytes only
   for (uint16_t r = 0; r < n; ++r) {
     ASSERT_EQ(size_t(32), names[r].size());

@@ -79,6 +79,39 @@ class _chunk_storage {
     return result;
   }
 
+  expected<std::vector<const_data_buffer>> restore_datas(
+      const std::vector<std::unordered_map<uint16_t, const_data_buffer>> &objects) {
+    const size_t count = objects.size();
+    std::vector<uint16_t> nodes;
+    std::vector<const uint8_t *> chunks;
+    std::vector<uint64_t> sizes(count), out_sizes(count);
+    for (size_t o = 0; o < count; ++o) {  // the checks of restore_data (chunk_storage.cpp:65-77)
+      const auto &h = objects[o];
+      if (min_horcrux_ != h.size()) return make_unexpected<std::runtime_error>("Error at restoring data");
+      sizes[o] = h.begin()->second.size();
+      for (auto &p : h) {
+        if (sizes[o] != p.second.size()) return make_unexpected<std::runtime_error>("Error at restoring data");
+        nodes.push_back(p.first);
+        chunks.push_back(p.second.data());
+      }
+    }
+    std::vector<std::vector<uint8_t>> bufs(count);
+    std::vector<uint8_t *> outs(count);
+    for (size_t o = 0; o < count; ++o) {
+      bufs[o].resize(sizes[o] * min_horcrux_ ? sizes[o] * min_horcrux_ : 1);  // >= any restored length
+      outs[o] = bufs[o].data();
+      out_sizes[o] = bufs[o].size();
+    }
+    const int rc = vds_ec_restore16_host_batch(min_horcrux_, nodes.data(), chunks.data(), sizes.data(),
+                                               uint32_t(count), outs.data(), out_sizes.data(), 0, 0);
+    if (rc == VDS_EC_ERESTORE) return make_unexpected<std::runtime_error>("Fatal error at chunk_restore::restore");
+    if (rc != VDS_EC_OK) return make_unexpected<std::runtime_error>(vds_ec_strerror(rc));
+    std::vector<const_data_buffer> result;
+    result.reserve(count);
+    for (size_t o = 0; o < count; ++o) result.emplace_back(bufs[o].data(), out_sizes[o]);
+    return result;
+  }
+
   // chunk_storage.cpp:62-86: exactly k equal-size horcruxes.
   expected<const_data_buffer> restore_data(const std::unordered_map<uint16_t, const_data_buffer> &horcruxes) {
     if (min_horcrux_ != horcruxes.size()) return make_unexpected<std::runtime_error>("Error at restoring data");
@@ -100,6 +133,11 @@ class _chunk_storage {
 };
 
 chunk_storage::chunk_storage(uint16_t min_horcrux) : impl_(new _chunk_storage(min_horcrux)) {}
+
+expected<std::vector<const_data_buffer>> chunk_storage::restore_datas(
+    const std::vector<std::unordered_map<uint16_t, const_data_buffer>> &objects) {
+  return impl_->restore_datas(objects);
+}
 chunk_storage::~chunk_storage() { delete impl_; }
 
 expected<const_data_buffer> chunk_storage::generate_replica(uint16_t replica, const void *data, size_t size) {

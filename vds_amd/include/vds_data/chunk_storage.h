@@ -31,6 +31,12 @@ class chunk_storage {
                                                              const void *data, size_t size,
                                                              std::vector<const_data_buffer> &hashes);
 
+  // Batched restore_data: object o from the k equal-size horcruxes of
+  // objects[o] (one device pass per object over every GPU, pinned staging);
+  // the same results and errors as restore_data per object.
+  expected<std::vector<const_data_buffer>> restore_datas(
+      const std::vector<std::unordered_map<uint16_t, const_data_buffer>> &objects);
+
   // Repair without materialising the object (sync_process.cpp:313-335 does
   // restore_data + generate_replica): replicas `targets` from exactly
   // min_horcrux equal-size horcruxes, byte-identical to that route.

@@ -191,12 +191,15 @@ int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void
 /* Which kernel path a device call with these parameters takes: 3 = syndrome
  * restore (erasure-pattern-independent XOR programs, survivors within
  * 0..k+k/4-1) for the full tiles, 2 = bit-sliced fast path for the full tiles
- * (+ generic tail), 1 = generic path only.  VDS_EC_RESTORE_PATH=bs in the
+ * (+ generic tail; objects under one tile whose stripes are whole 512-stripe
+ * groups ride it in batches), 1 = generic path only.  VDS_EC_RESTORE_PATH=bs in the
  * environment disables path 3 (for A/B measurements).                       */
 int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint64_t size);
 int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size);
 /* 3 = the regenerate rides the syndrome kernel (every target an erased point
- * of a compiled (k, n)) for the full tiles, 1 = generic path only.          */
+ * of a compiled (k, n)) for the full tiles, 2 = the runtime-coefficient
+ * bit-sliced kernel (k in {16, 32}, at most k targets, >= 512 full stripes),
+ * 1 = generic path only.                                                    */
 int vds_ec_regenerate16_path(uint16_t k, const uint16_t *nodes, const uint16_t *targets, uint32_t ntargets,
                              uint64_t chunk_size);
 

@@ -325,6 +325,7 @@ def test_restore_path_selection(ec):
     assert _path(16, list(range(4, 20)), 2 * 100 + 2) == 1         # no full tile
     assert _path(32, list(range(8, 40)), 2 * 2048 * 32 + 2) in (2, 3)
     assert _path(5, list(range(5)), L) == 1
+    assert _path(32, list(range(32, 64)), 2 * 1024 + 2) == 2       # live shape: 64 KiB objects, stream mode
 
 
 def test_restore_device_batched(ec):

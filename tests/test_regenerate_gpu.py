@@ -56,7 +56,7 @@ def test_regenerate_fast_path_selected(chunk):
     t_in = np.array([5, 0], dtype=np.uint16)
     t_out = np.array([5, 21], dtype=np.uint16)
     assert p(k, nodes.ctypes.data_as(_lib.u16p), t_in.ctypes.data_as(_lib.u16p), 2, L) == 3
-    assert p(k, nodes.ctypes.data_as(_lib.u16p), t_out.ctypes.data_as(_lib.u16p), 2, L) == 1
+    assert p(k, nodes.ctypes.data_as(_lib.u16p), t_out.ctypes.data_as(_lib.u16p), 2, L) == 2  # runtime-coefficient kernel
     assert p(k, nodes.ctypes.data_as(_lib.u16p), t_in.ctypes.data_as(_lib.u16p), 2, 1000) == 1
 
 
@@ -97,6 +97,47 @@ def test_regenerate_device_batched_strided(chunk):
     for i, t in enumerate(erased):
         for o in range(count):
             assert np.array_equal(host[i, o, :L], reps[t, o, :L]), f"replica {t} object {o}"
+            assert not host[i, o, L:].any(), "wrote past the replica"
+
+
+@pytest.mark.parametrize("k,n,size,count,erased,targets,path", [
+    # the live shape (dht_network.h:22-25): 64 KiB objects, tiles straddle objects, last object generic
+    (32, 64, 65536, 5, list(range(1, 64, 2)), [1, 3, 63, 33, 0], 2),
+    (32, 64, 2 * 65536 + 3000, 3, list(range(32, 64)), list(range(32, 64)), 2),  # whole tiles + generic rest
+    (16, 20, 3 * 65536 + 77, 2, [1, 2, 3, 4], [1, 2, 3, 4, 30], 2),           # a target beyond n
+    (16, 20, 4 * 65536, 3, [16, 17, 18, 19], [0, 19, 16], 2),                 # a surviving point as target
+    (16, 20, 4 * 65536, 3, [0, 5, 10, 15], [15, 0], 3),                       # syndrome kernel
+])
+def test_regenerate_device_fast_paths(chunk, k, n, size, count, erased, targets, path):
+    """Every fast regenerate path against the reference route (restore, then
+    encode of the target) on batches of objects: bit-exact, trailers included,
+    nothing written past a replica."""
+    import torch
+    from vds_amd import _lib
+    L = chunk.replica_size(k, size)
+    objs = [O.splitmix(SEED + 300 + 7 * o + k, size) for o in range(count)]
+    nodes = [r for r in range(n) if r not in erased][:k]
+    stride = L + 4
+    reps = np.zeros((k, count, stride), dtype=np.uint8)
+    want = np.zeros((len(targets), count, L), dtype=np.uint8)
+    for o, d in enumerate(objs):
+        for j, r in enumerate(nodes):
+            reps[j, o, :L] = O.encode(k, r, d)
+        for i, t in enumerate(targets):
+            want[i, o] = O.encode(k, t, d)
+    nd = np.array(nodes, dtype=np.uint16)
+    tg = np.array(targets, dtype=np.uint16)
+    assert _lib.lib().vds_ec_regenerate16_path(k, nd.ctypes.data_as(_lib.u16p), tg.ctypes.data_as(_lib.u16p),
+                                               len(targets), L) == path
+    dev = torch.from_numpy(reps).cuda()
+    out = torch.zeros((len(targets), count, L + 8), dtype=torch.uint8, device="cuda")
+    chunk.regenerate_device(k, nodes, [dev[j].data_ptr() for j in range(k)], L, stride, count, targets,
+                            [out[i].data_ptr() for i in range(len(targets))], L + 8)
+    torch.cuda.synchronize()
+    host = out.cpu().numpy()
+    for i, t in enumerate(targets):
+        for o in range(count):
+            assert np.array_equal(host[i, o, :L], want[i, o]), f"replica {t} object {o}"
             assert not host[i, o, L:].any(), "wrote past the replica"
 
 

@@ -81,6 +81,11 @@ struct FastRestoreArgs {
   // k x k inverse, row-major, two coefficients per dword (low half = even
   // column) so the wave-uniform reads are scalar s_load_dword.
   uint32_t matrix2[kMaxFastK * kMaxFastK / 2];
+  // regenerate mode (k_restore_bs<..., true>): output m < nt is replica
+  // bytes (cells in stripe order) at regen[m] + o * out_stride, the matrix
+  // rows are V_targets V_S^{-1} (rows nt.. zero)
+  uint8_t *regen[kMaxFastK];
+  uint32_t nt;
 };
 
 // Erasure-pattern-independent restore (k_restore_syn<K,N>): survivors are K
@@ -140,7 +145,7 @@ hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s);
 // Returns hipErrorNotSupported when no bit-sliced instantiation exists for (k, n).
 hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, hipStream_t s);
 bool has_encode_fast(uint32_t k, uint32_t n);
-hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t s);
+hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t s, bool regen = false);
 bool has_restore_fast(uint32_t k);
 // SHA-256 of count messages of len bytes at base + j * stride -> digests + 32 j (sha256.hip).
 hipError_t launch_sha256(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count, uint8_t *digests,

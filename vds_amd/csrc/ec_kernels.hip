@@ -555,7 +555,7 @@ __device__ __forceinline__ void restore_load(u32x4 (&Q)[RestoreShape<K>::kPerWav
   }
 }
 
-template <int K, bool STREAM>
+template <int K, bool STREAM, bool REGEN>
 __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(FastRestoreArgs a) {
   using S = RestoreShape<K>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -603,6 +603,29 @@ __global__ __launch_bounds__((RestoreShape<K>::kThreads), 2) void k_restore_bs(F
         c[s] = (a.matrix2[idx >> 1] >> (16 * (idx & 1))) & 0xFFFFu;
       }
       plane_mac_rt<S::kPerWave>(acc, y, c);
+    }
+    if constexpr (REGEN) {
+      // ---- regenerate: output m is replica regen[m]'s cells for the same
+      // stripes the survivors were loaded from; undo the load transpose and
+      // store with the load's addressing (1 KiB per wave-instruction)
+#pragma unroll
+      for (int s = 0; s < S::kPerWave; ++s) {
+        const uint32_t m = wave * S::kPerWave + s;
+        if (m >= a.nt) continue;
+        uint32_t W[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) W[b ^ 8] = acc[s].p[b];
+        transpose16x2(W);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t o, r;
+          restore_group(a, tile, STREAM ? q : 0, o, r);
+          uint8_t *dst = a.regen[m] + (uint64_t)o * a.out_stride + 1024ull * (STREAM ? r : r + q) + 16 * lane;
+          *reinterpret_cast<u32x4 *>(dst) = u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]};
+        }
+      }
+      __syncthreads();
+      continue;
     }
     // ---- back to big-endian cells: word group w' = cells (2w', 2w'+1)
 #pragma unroll
@@ -1343,12 +1366,12 @@ hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, h
   return hipErrorNotSupported;
 }
 
-template <int K, bool STREAM>
+template <int K, bool STREAM, bool REGEN>
 static hipError_t launch_restore_bs_k(const FastRestoreArgs &a, hipStream_t s) {
   using S = RestoreShape<K>;
   static bool configured = false;
   if (!configured) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_restore_bs<K, STREAM>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_restore_bs<K, STREAM, REGEN>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, S::kLdsBytes);
     if (e != hipSuccess) return e;
     configured = true;
@@ -1357,16 +1380,22 @@ static hipError_t launch_restore_bs_k(const FastRestoreArgs &a, hipStream_t s) {
   int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
   if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_restore_bs<K, STREAM>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  hipLaunchKernelGGL((k_restore_bs<K, STREAM, REGEN>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
   return hipGetLastError();
 }
 
 bool has_restore_fast(uint32_t k) { return k == 16 || k == 32; }
 
-hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t s) {
+template <int K>
+static hipError_t launch_restore_bs_kk(const FastRestoreArgs &a, hipStream_t s, bool regen) {
   const bool stream = a.groups_per_obj % 4 != 0;
-  if (k == 16) return stream ? launch_restore_bs_k<16, true>(a, s) : launch_restore_bs_k<16, false>(a, s);
-  if (k == 32) return stream ? launch_restore_bs_k<32, true>(a, s) : launch_restore_bs_k<32, false>(a, s);
+  if (regen) return stream ? launch_restore_bs_k<K, true, true>(a, s) : launch_restore_bs_k<K, false, true>(a, s);
+  return stream ? launch_restore_bs_k<K, true, false>(a, s) : launch_restore_bs_k<K, false, false>(a, s);
+}
+
+hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t s, bool regen) {
+  if (k == 16) return launch_restore_bs_kk<16>(a, s, regen);
+  if (k == 32) return launch_restore_bs_kk<32>(a, s, regen);
   return hipErrorNotSupported;
 }
 

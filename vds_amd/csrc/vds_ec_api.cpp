@@ -529,6 +529,28 @@ int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint
   if (rc) return rc;
   const uint64_t T = (chunk_size - 2) / cb;
   uint64_t fast_stripes = 0;
+  // coef[i][j] = sum_m t_i^m inv[m][j]  (P_m = sum_j inv[m][j] c_j): replica
+  // t_i as a combination of the survivors
+  auto coefs = [&](uint32_t base, uint32_t cnt) {
+    std::vector<uint16_t> coef((size_t)cnt * k, 0);
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint32_t t = targets[base + i];
+      for (uint32_t m = 0; m < k; ++m) {
+        const uint32_t tm = cb == 2 ? gf16_vandermonde(t, m) : (m == 0 ? 1u : gf8_pow(t, m));
+        if (!tm) continue;
+        for (uint32_t j = 0; j < k; ++j) {
+          const uint32_t v = inv[(size_t)m * k + j];
+          coef[(size_t)i * k + j] ^= (uint16_t)(cb == 2 ? gf16_mul(tm, v) : gf8_mul(tm, v));
+        }
+      }
+    }
+    return coef;
+  };
+  // objects [o0, o0 + cnt) still need cells [t_begin, T) and the trailer
+  struct Part {
+    uint64_t o0, cnt, t_begin;
+  };
+  Part parts[3] = {{0, count, 0}, {0, 0, 0}, {0, 0, 0}};
   SynRestoreArgs sa{};
   uint32_t syn_n = 0;
   if (cb == 2 && plan_restore_syn(k, nodes, sa, &syn_n)) {
@@ -554,6 +576,38 @@ int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint
       hipError_t e = launch_restore_syn(k, syn_n, sa, s, true);
       if (e != hipSuccess) return hip_status(e);
       fast_stripes = tiles * kTileStripes;
+      parts[0].t_begin = fast_stripes;
+    }
+  }
+  if (!fast_stripes && cb == 2 && has_restore_fast(k) && nt <= k) {
+    // any survivors, any targets (e.g. the live n = 64 shape): the
+    // runtime-coefficient bit-sliced kernel with the nt x k combination rows,
+    // over 512-stripe groups (tiles of four may straddle objects when 512 | T)
+    const uint64_t gpo = T % 512 == 0 ? T / 512 : 4 * (T / kTileStripes);
+    const uint64_t total = gpo * count / 4;
+    if (gpo > 0 && gpo <= 0xFFFFFFFFull && total > 0 && total <= 0xFFFFFFFFull) {
+      FastRestoreArgs fa{};
+      for (uint32_t j = 0; j < k; ++j) fa.chunks[j] = chunks[j];
+      fa.chunk_stride = chunk_stride;
+      fa.out_stride = out_stride;
+      fa.groups_per_obj = (uint32_t)gpo;
+      fa.total_tiles = (uint32_t)total;
+      fa.nt = nt;
+      for (uint32_t i = 0; i < nt; ++i) fa.regen[i] = outs[i];
+      const std::vector<uint16_t> coef = coefs(0, nt);
+      for (size_t x = 0; x < coef.size(); ++x) fa.matrix2[x >> 1] |= uint32_t(coef[x]) << (16 * (x & 1));
+      hipError_t e = launch_restore_fast(k, fa, s, true);
+      if (e != hipSuccess) return hip_status(e);
+      if (gpo % 4 == 0) {
+        fast_stripes = 512 * gpo;
+        parts[0].t_begin = fast_stripes;
+      } else {  // stream: the first 2048 * total stripes of the objects taken as one stream
+        const uint64_t fast_total = (uint64_t)kTileStripes * total, o_full = fast_total / T;
+        fast_stripes = fast_total;
+        parts[0] = {0, o_full, T};
+        parts[1] = {o_full, o_full < count ? 1u : 0u, fast_total - o_full * T};
+        parts[2] = {o_full + 1, o_full + 1 < count ? count - o_full - 1 : 0, 0};
+      }
     }
   }
   // generic path: the remaining cells and the trailers, <= 64 targets per launch
@@ -566,23 +620,8 @@ int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint
   for (uint32_t base = 0; base < nt && e == hipSuccess; base += kMaxLaunchReplicas) {
     RegenArgs ga{};
     ga.nt = std::min<uint32_t>(nt - base, kMaxLaunchReplicas);
-    if (tmp_table)
-      ga.chunk_table = static_cast<const uint8_t *const *>(tmp_table);
-    else
-      for (uint32_t j = 0; j < k; ++j) ga.chunk_ptr[j] = chunks[j];
-    // coef[i][j] = sum_m t_i^m inv[m][j]  (P_m = sum_j inv[m][j] c_j)
-    std::vector<uint16_t> coef((size_t)ga.nt * k, 0);
-    for (uint32_t i = 0; i < ga.nt; ++i) {
-      const uint32_t t = targets[base + i];
-      for (uint32_t m = 0; m < k; ++m) {
-        const uint32_t tm = cb == 2 ? gf16_vandermonde(t, m) : (m == 0 ? 1u : gf8_pow(t, m));
-        if (!tm) continue;
-        for (uint32_t j = 0; j < k; ++j) {
-          const uint32_t v = inv[(size_t)m * k + j];
-          coef[(size_t)i * k + j] ^= (uint16_t)(cb == 2 ? gf16_mul(tm, v) : gf8_mul(tm, v));
-        }
-      }
-    }
+    if (tmp_table) ga.chunk_table = static_cast<const uint8_t *const *>(tmp_table);
+    const std::vector<uint16_t> coef = coefs(base, ga.nt);
     if (coef.size() <= (size_t)kInlineCoef) {
       for (size_t x = 0; x < coef.size(); ++x) ga.coef_inline[x >> 1] |= uint32_t(coef[x]) << (16 * (x & 1));
     } else {
@@ -597,15 +636,24 @@ int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint
     }
     if (e != hipSuccess) break;
     ga.chunk_stride = chunk_stride;
-    ga.count = count;
     ga.k = k;
     ga.cell_bytes = cb;
-    ga.t_begin = fast_stripes;
-    ga.t_count = T - fast_stripes;
     ga.T = T;
-    for (uint32_t i = 0; i < ga.nt; ++i) ga.outs[i] = outs[base + i];
     ga.out_stride = out_stride;
-    e = launch_regen_generic(ga, s);
+    for (const Part &pt : parts) {
+      if (e != hipSuccess || pt.cnt == 0) continue;
+      if (tmp_table && pt.o0) {  // (k > 64: never with a fast path, so o0 == 0)
+        e = hipErrorInvalidValue;
+        break;
+      }
+      if (!tmp_table)
+        for (uint32_t j = 0; j < k; ++j) ga.chunk_ptr[j] = chunks[j] + pt.o0 * chunk_stride;
+      for (uint32_t i = 0; i < ga.nt; ++i) ga.outs[i] = outs[base + i] + pt.o0 * out_stride;
+      ga.count = (uint32_t)pt.cnt;
+      ga.t_begin = pt.t_begin;
+      ga.t_count = T - pt.t_begin;
+      e = launch_regen_generic(ga, s);
+    }
   }
   if (tmp_table || tmp_coef) {
     const hipError_t se = hipStreamSynchronize(s);
@@ -1170,13 +1218,20 @@ int vds_ec_regenerate16_path(uint16_t k, const uint16_t *nodes, const uint16_t *
   if (k == 0 || !nodes || (ntargets && !targets) || chunk_size < 2) return 0;
   SynRestoreArgs sa{};
   uint32_t n = 0;
-  if ((chunk_size - 2) / 2 < kTileStripes || !plan_restore_syn(k, nodes, sa, &n)) return 1;
-  for (uint32_t i = 0; i < ntargets; ++i) {
+  const uint64_t T = (chunk_size - 2) / 2;
+  bool syn = T >= kTileStripes && plan_restore_syn(k, nodes, sa, &n);
+  for (uint32_t i = 0; syn && i < ntargets; ++i) {  // (mirrors regenerate_device's choice)
     bool hit = false;
-    for (uint32_t w = 0; w < n - k; ++w) hit |= sa.erased[w] == targets[i];
-    if (!hit) return 1;
+    for (uint32_t w = 0; w < n - k; ++w)
+      if (sa.erased[w] == targets[i] && !sa.regen[w]) {
+        sa.regen[w] = reinterpret_cast<uint8_t *>(1);
+        hit = true;
+      }
+    syn = hit;
   }
-  return 3;
+  if (syn) return 3;
+  const uint64_t gpo = T % 512 == 0 ? T / 512 : 4 * (T / kTileStripes);
+  return (has_restore_fast(k) && ntargets <= k && gpo > 0) ? 2 : 1;
 }
 
 int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void *stream) {
@@ -1196,8 +1251,11 @@ int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint6
 }
 
 int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size) {
-  const uint64_t tiles = (k && chunk_size >= 2) ? ((chunk_size - 2) / 2) / kTileStripes : 0;
-  if (tiles == 0) return 1;
+  const uint64_t T = (k && chunk_size >= 2) ? (chunk_size - 2) / 2 : 0;  // full stripes of an unpadded object
+  const uint64_t tiles = T / kTileStripes;
+  // objects under one tile: stream mode of the bit-sliced kernel when their
+  // stripes are whole 512-stripe groups (batches of >= 2048 / T objects)
+  if (tiles == 0) return (T > 0 && T % 512 == 0 && has_restore_fast(k)) ? 2 : 1;
   SynRestoreArgs sa{};
   uint32_t n = 0;
   if (plan_restore_syn(k, nodes, sa, &n)) return 3;

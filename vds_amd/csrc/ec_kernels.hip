@@ -723,8 +723,8 @@ constexpr bool kSynSameCode = VDS_SYN_SAME_CODE;
 #ifndef VDS_DIAG_STAMPS
 #define VDS_DIAG_STAMPS 0
 #endif
-constexpr int kStampPhases = 20;
 #if VDS_DIAG_STAMPS
+constexpr int kStampPhases = 20;
 constexpr int kStampSlots = 4096 * 4 * kStampPhases;
 __device__ unsigned long long g_syn_stamps[kStampSlots];
 struct Stamps {

@@ -213,13 +213,23 @@ VDS_INLINE Plane16 plane_mul_rt(const Plane16 &a, uint32_t c) {
 }
 
 // acc[s] ^= c[s] * y for NS runtime constants, sharing the y * x^b chain:
-// y*c = sum_b c_b (y x^b).  Cost: 45 XOR + 16*16*NS masked XOR.
+// y*c = sum_b c_b (y x^b).  Cost: 45 XOR + 16*16*NS masked XOR.  The
+// coefficients are wave-uniform (SGPRs); each bit's all-ones/zero mask is
+// moved to a VGPR first: a v_bitop3_b32 reading an SGPR issues at ~0.6 of
+// the all-VGPR rate (profiles/round1/valu_op_rates.txt), one v_mov per mask
+// buys sixteen full-rate bitop3s.
 template <int NS>
 VDS_INLINE void plane_mac_rt(Plane16 (&acc)[NS], Plane16 y, const uint32_t (&c)[NS]) {
 #pragma unroll
   for (int b = 0; b < 16; ++b) {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) plane_xor_masked(acc[s], y, 0u - ((c[s] >> b) & 1u));
+    for (int s = 0; s < NS; ++s) {
+      uint32_t m = 0u - ((c[s] >> b) & 1u);
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(VDS_MAC_SGPR_MASK)
+      asm("v_mov_b32 %0, %1" : "=v"(m) : "s"(m));
+#endif
+      plane_xor_masked(acc[s], y, m);
+    }
     if (b < 15) y = plane_mulx(y);
   }
 }

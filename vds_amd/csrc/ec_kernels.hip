@@ -799,6 +799,10 @@ __device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t 
 #define VDS_SYN_REC 2
 #endif
 
+#ifndef VDS_SYN_CFENCE  // 1: one scheduling fence per stage-C term
+#define VDS_SYN_CFENCE 0
+#endif
+
 #ifndef VDS_SYN_GM  // 1: interpolation by one additive-FFT level + half-size programs; 0: one 16-point program
 #define VDS_SYN_GM 1
 #endif
@@ -849,6 +853,9 @@ __device__ __forceinline__ void syn_gm_stage_c(const SynLds &L, uint32_t (&cells
         syn_get_point(L, t, v);
 #pragma unroll
         for (int b = 0; b < 16; ++b) acc[b] ^= v[b];
+#if VDS_SYN_CFENCE
+        __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting every term's reads
+#endif
       }
     }
 #pragma unroll
@@ -936,6 +943,19 @@ void k_restore_syn(SynRestoreArgs a) {
       for (int q = 0; q < 4; ++q) Q[s][q] = *reinterpret_cast<const u32x4 *>(src + 1024 * q);
     }
   };
+  // The next tile's survivors, or zeros past the last tile: both paths define
+  // Q, so the values consumed by this tile's stage 1 die there instead of
+  // staying live (as loop-carried state) through the programs until the load
+  auto prefetch = [&](uint32_t t) {
+    if (t < a.total_tiles) {
+      load(t);
+    } else {
+#pragma unroll
+      for (int s = 0; s < S::kLoadPer; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Q[s][q] = u32x4{0u, 0u, 0u, 0u};
+    }
+  };
   Stamps st;
   st.init();
   // k = 32 (one 160 KiB workgroup per CU): the prefetched survivors would be
@@ -943,6 +963,9 @@ void k_restore_syn(SynRestoreArgs a) {
   // issued after the interpolation instead and land under the staging and
   // stores (REGEN has no interpolation and keeps the early issue)
   constexpr bool kLateLoad = VDS_SYN_LATE && K == 32 && !REGEN && VDS_SYN_GM;
+  // VDS_SYN_LATE 2: issued inside the output staging, once the first word
+  // group's cells are dead (no spills of loop-carried state around them)
+  constexpr bool kStageLoad = kLateLoad && VDS_SYN_LATE == 2;
   if (blockIdx.x < a.total_tiles) load(blockIdx.x);
   for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
     const uint32_t o = tile / a.tiles_per_obj;
@@ -985,7 +1008,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #else
       P::syndrome(kSynSameCode ? 1 : wave, L, t.p);
 #endif
-      if (!kLateLoad && tile + gridDim.x < a.total_tiles) load(tile + gridDim.x);
+      if (!kLateLoad) prefetch(tile + gridDim.x);
       st.mark(2);
       // M <= 4: all products before the barrier (their walk overlaps the
       // slower waves' syndromes); M = 8: four at a time after it (eight
@@ -1041,7 +1064,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #else
       P::syndrome(kSynSameCode ? 1 : wave, L, syn);
 #endif
-      if (tile + gridDim.x < a.total_tiles) load(tile + gridDim.x);
+      prefetch(tile + gridDim.x);
       __syncthreads();  // every wave is done reading the zeroed erased planes
 #pragma unroll
       for (int r = 0; r < S::kSynRows; r += 4) {
@@ -1106,7 +1129,7 @@ void k_restore_syn(SynRestoreArgs a) {
       for (int r = 0; r < 16 * S::kCells; ++r) cells[r] = lane * r;
 #elif VDS_SYN_GM
       syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
-      if (kLateLoad && tile + gridDim.x < a.total_tiles) load(tile + gridDim.x);
+      if (kLateLoad && !kStageLoad) prefetch(tile + gridDim.x);
 #else
       P::interp(kSynSameCode ? 1 : wave, L, cells);
 #endif
@@ -1183,6 +1206,7 @@ void k_restore_syn(SynRestoreArgs a) {
             *(__attribute__((address_space(3))) uint32_t *)(w0 + (slot >> 3) * (32768 + 512) + (slot & 7) * 64) =
                 rows[pi];
           }
+          if (kStageLoad && g == 0) prefetch(tile + gridDim.x);
         }
         st.mark(15);
         __syncthreads();

@@ -286,6 +286,24 @@ __device__ __forceinline__ TilePos tile_pos(const FastEncodeArgs &a, uint32_t ti
 // 2s + 128j + 1, so output word j (low half = slot j, high half = slot 16 + j,
 // transpose16x2) is the 4 bytes of stripes 2s, 2s+1 of group j: one dword
 // store per word, 256 contiguous bytes per wave-instruction.
+// Streaming (non-temporal) global accesses for the data path, A/B switch:
+// VDS_NT bit 1 = encode replica stores, 2 = encode object loads, 4 = restore
+// survivor loads, 8 = restore / regenerate stores.  Every byte is read or
+// written exactly once, so nothing is lost by not keeping it in L2.
+#ifndef VDS_NT
+#define VDS_NT 13  // A/B (512 x 64 MiB, 3 rounds): 0 -> 840, 13 -> 859, 15 -> 856 GiB/s encode+repair
+#endif
+template <int BIT, class T>
+__device__ __forceinline__ T g_ld(const void *p) {
+  if constexpr ((VDS_NT & BIT) != 0) return __builtin_nontemporal_load(reinterpret_cast<const T *>(p));
+  else return *reinterpret_cast<const T *>(p);
+}
+template <int BIT, class T>
+__device__ __forceinline__ void g_st(void *p, T v) {
+  if constexpr ((VDS_NT & BIT) != 0) __builtin_nontemporal_store(v, reinterpret_cast<T *>(p));
+  else *reinterpret_cast<T *>(p) = v;
+}
+
 template <bool STREAM>
 __device__ __forceinline__ void store_replica_groups(const Plane16 &acc, uint8_t *rep, const FastEncodeArgs &a,
                                                      TilePos tp, int lane, const BitMasks &bm) {
@@ -301,12 +319,12 @@ __device__ __forceinline__ void store_replica_groups(const Plane16 &acc, uint8_t
   if constexpr (!STREAM) {  // whole tiles per object: one base, immediate offsets
     uint32_t *b = reinterpret_cast<uint32_t *>(rep + (uint64_t)tp.o * a.out_stride + 256u * tp.q + 4 * lane);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) b[64 * j] = rows[j];
+    for (int j = 0; j < 16; ++j) g_st<1>(b + 64 * j, rows[j]);
   } else {
     uint32_t o = tp.o, q = tp.q;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      *reinterpret_cast<uint32_t *>(rep + (uint64_t)o * a.out_stride + 256u * q + 4 * lane) = rows[j];
+      g_st<1>(rep + (uint64_t)o * a.out_stride + 256u * q + 4 * lane, rows[j]);
       if (++q == a.groups_per_obj) {
         q = 0;
         ++o;
@@ -422,12 +440,12 @@ __device__ __forceinline__ void encode_load16(u32x4 (&V)[16], const FastEncodeAr
   if constexpr (!STREAM) {  // whole tiles per object
     const uint8_t *src = a.in + (uint64_t)o * a.in_stride + (uint64_t)q * 128 * (2 * K) + lane_off;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) V[j] = *reinterpret_cast<const u32x4 *>(src + (uint64_t)j * 128 * (2 * K));
+    for (int j = 0; j < 16; ++j) V[j] = g_ld<2, u32x4>(src + (uint64_t)j * 128 * (2 * K));
     return;
   }
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    V[j] = *reinterpret_cast<const u32x4 *>(a.in + (uint64_t)o * a.in_stride + (uint64_t)q * 128 * (2 * K) + lane_off);
+    V[j] = g_ld<2, u32x4>(a.in + (uint64_t)o * a.in_stride + (uint64_t)q * 128 * (2 * K) + lane_off);
     if (++q == a.groups_per_obj) {
       q = 0;
       ++o;
@@ -795,6 +813,10 @@ __device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t 
 #define VDS_SYN_LATE 1
 #endif
 
+#ifndef VDS_SYN_LATE16  // 1: k = 16 also issues the next tile's loads after the interpolation (A/B)
+#define VDS_SYN_LATE16 0
+#endif
+
 #ifndef VDS_SYN_REC  // 2: scatter recovery with LDS XOR atomics; 1: gather (parks the syndromes)
 #define VDS_SYN_REC 2
 #endif
@@ -940,7 +962,7 @@ void k_restore_syn(SynRestoreArgs a) {
     for (int s = 0; s < S::kLoadPer; ++s) {
       const uint8_t *src = a.chunks[wave * S::kLoadPer + s] + (uint64_t)ob * a.chunk_stride + 2 * st0 + 16 * lane;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Q[s][q] = *reinterpret_cast<const u32x4 *>(src + 1024 * q);
+      for (int q = 0; q < 4; ++q) Q[s][q] = g_ld<4, u32x4>(src + 1024 * q);
     }
   };
   // The next tile's survivors, or zeros past the last tile: both paths define
@@ -962,7 +984,7 @@ void k_restore_syn(SynRestoreArgs a) {
   // live across the syndrome and stage-B programs, which then spill; they are
   // issued after the interpolation instead and land under the staging and
   // stores (REGEN has no interpolation and keeps the early issue)
-  constexpr bool kLateLoad = VDS_SYN_LATE && K == 32 && !REGEN && VDS_SYN_GM;
+  constexpr bool kLateLoad = VDS_SYN_LATE && (K == 32 || VDS_SYN_LATE16) && !REGEN && VDS_SYN_GM;
   // VDS_SYN_LATE 2: issued inside the output staging, once the first word
   // group's cells are dead (no spills of loop-carried state around them)
   constexpr bool kStageLoad = kLateLoad && VDS_SYN_LATE == 2;
@@ -1117,7 +1139,7 @@ void k_restore_syn(SynRestoreArgs a) {
         uint8_t *dst = a.regen[wave] + (uint64_t)o * a.regen_stride + 2 * stripe0 + 16 * lane;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          *reinterpret_cast<u32x4 *>(dst + 1024 * q) = u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]};
+          g_st<8>(dst + 1024 * q, u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]});
       }
       __syncthreads();  // every wave is done with this tile's planes
       continue;
@@ -1177,7 +1199,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #if VDS_DIAG_RES == 2
           if (a.out_stride == 1)
 #endif
-          *reinterpret_cast<u32x4 *>(g0 + 1024 * i) = v;
+          g_st<8>(g0 + 1024 * i, v);
         }
         st.mark(17);
       } else if constexpr (K == 32) {
@@ -1224,7 +1246,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #if VDS_DIAG_RES == 2
           if (a.out_stride == 1)
 #endif
-          *reinterpret_cast<u32x4 *>(g0 + 1024 * i) = u32x4{v0[0], v0[1], v1[0], v1[1]};
+          g_st<8>(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]});
         }
         st.mark(17);
       } else {

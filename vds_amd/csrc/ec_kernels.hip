@@ -289,7 +289,10 @@ __device__ __forceinline__ TilePos tile_pos(const FastEncodeArgs &a, uint32_t ti
 // Streaming (non-temporal) global accesses for the data path, A/B switch:
 // VDS_NT bit 1 = encode replica stores, 2 = encode object loads, 4 = restore
 // survivor loads, 8 = restore / regenerate stores.  Every byte is read or
-// written exactly once, so nothing is lost by not keeping it in L2.
+// written exactly once, so nothing is lost by not keeping it in L2.  Only for
+// whole-line wave accesses: k_restore_bs with non-temporal 4-byte strided
+// stores and loads measured 3.4x slower (live shape repair 212 -> 79 GiB/s),
+// so it keeps plain accesses.
 #ifndef VDS_NT
 #define VDS_NT 13  // A/B (512 x 64 MiB, 3 rounds): 0 -> 840, 13 -> 859, 15 -> 856 GiB/s encode+repair
 #endif

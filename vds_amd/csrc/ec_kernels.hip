@@ -348,9 +348,16 @@ __device__ __forceinline__ void store_rep(const Plane16 &acc, uint8_t *rep, cons
     store_replica_groups<STREAM>(acc, rep, a, tp, lane, bm);
 }
 
-#ifndef VDS_ENC_PASS  // replicas evaluated per pass over the tile's cells
+#ifndef VDS_ENC_PRIO  // wave priority while a pass issues its stores (A/B; 0 = off)
+#define VDS_ENC_PRIO 2  // A/B (512 objects, 2 rounds): encode 1881-1895 -> 1917-1918 GiB/s
+#endif
+
+#ifndef VDS_ENC_PASS  // replicas evaluated per pass over the tile's cells (k = 4, 32)
 #define VDS_ENC_PASS 3
 #endif
+#ifndef VDS_ENC_PASS16  // the same for k = 16 (A/B with the non-temporal, prioritised stores, 512
+#define VDS_ENC_PASS16 5  // objects, 2 rounds: 1 -> 1740, 2 -> 1825, 3 -> 1867, 5 -> 1914 GiB/s encode;
+#endif                    // 5 at k = 32 spills)
 
 // One pass: Horner for plan slots S0 .. S0+PR-1 over cells K-1 .. 0, then the
 // stores.  Two Horner steps per iteration, so the accumulators alternate
@@ -388,18 +395,21 @@ __device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const Fa
     rows_step<K, N, RPW, WV, W, S0, PR>(A, B, xb);
   }
   rows_step<K, N, RPW, WV, W, S0, PR>(A, A, xa);  // cell 0 (each step returns a fresh value)
+  if constexpr (VDS_ENC_PRIO > 0) __builtin_amdgcn_s_setprio(VDS_ENC_PRIO);
 #pragma unroll
   for (int s = 0; s < PR; ++s) {
     const int r = S0 + s < RPW ? S::kPlan.rep[W][S0 + s] : -1;
     if (r == 0) store_rep<S::kMap, ST>(xa, a.outs[0], a, tp, lane, bm);
     if (r > 0) store_rep<S::kMap, ST>(A[s], a.outs[r], a, tp, lane, bm);
   }
+  if constexpr (VDS_ENC_PRIO > 0) __builtin_amdgcn_s_setprio(0);
 }
 
 template <int K, int N, int RPW, int WV, int W, bool ST, int S0 = 0>
 __device__ __forceinline__ void encode_wave_group(const uint32_t *set_planes, const FastEncodeArgs &a, TilePos tp,
                                                   int lane, const BitMasks &bm) {
-  constexpr int PR = VDS_ENC_PASS < RPW ? VDS_ENC_PASS : RPW;
+  constexpr int kPass = K == 16 ? VDS_ENC_PASS16 : VDS_ENC_PASS;
+  constexpr int PR = kPass < RPW ? kPass : RPW;
   if constexpr (S0 < RPW) {
     encode_pass<K, N, RPW, WV, W, S0, PR, ST>(set_planes, a, tp, lane, bm);
     encode_wave_group<K, N, RPW, WV, W, ST, S0 + PR>(set_planes, a, tp, lane, bm);
@@ -816,6 +826,10 @@ __device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t 
 #define VDS_SYN_LATE 1
 #endif
 
+#ifndef VDS_SYN_PRIO  // wave priority while issuing the survivor loads and the copy-out stores (A/B; 0 = off)
+#define VDS_SYN_PRIO 0  // A/B: 2 measured the same as 0 (repair 1598-1602 vs 1604-1606)
+#endif
+
 #ifndef VDS_SYN_LATE16  // 1: k = 16 also issues the next tile's loads after the interpolation (A/B)
 #define VDS_SYN_LATE16 0
 #endif
@@ -973,7 +987,9 @@ void k_restore_syn(SynRestoreArgs a) {
   // staying live (as loop-carried state) through the programs until the load
   auto prefetch = [&](uint32_t t) {
     if (t < a.total_tiles) {
+      if constexpr (VDS_SYN_PRIO > 0) __builtin_amdgcn_s_setprio(VDS_SYN_PRIO);
       load(t);
+      if constexpr (VDS_SYN_PRIO > 0) __builtin_amdgcn_s_setprio(0);
     } else {
 #pragma unroll
       for (int s = 0; s < S::kLoadPer; ++s)
@@ -1193,6 +1209,7 @@ void k_restore_syn(SynRestoreArgs a) {
         st.mark(16);
         // 16-byte chunk c = 64 (kChunks wave + i) + lane of the tile: stripe c/2, half c%2
         constexpr int kChunks = 64 / WV;  // 1 KiB pieces of the tile each wave writes
+        if constexpr (VDS_SYN_PRIO > 0) __builtin_amdgcn_s_setprio(VDS_SYN_PRIO);
         const lds_char *r0 =
             L.base + 1056u * kChunks * wave + 32u * (lane >> 1) + 16u * (lane >> 5) + 16u * (lane & 1);
         uint8_t *g0 = dst + stripe0 * (2 * K) + 1024u * kChunks * wave + 16u * lane;
@@ -1204,6 +1221,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #endif
           g_st<8>(g0 + 1024 * i, v);
         }
+        if constexpr (VDS_SYN_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         st.mark(17);
       } else if constexpr (K == 32) {
         // Stage as for k = 16 with 64-byte stripes and 8 bytes of padding

@@ -194,6 +194,8 @@ def test_fast_encode_object_stream(ec, k, n, size, count, pad):
     (16, list(range(20, 36)), 16384, 7),                   # runtime-coefficient kernel, 1 group per object
     (16, list(range(20, 36)), 3 * 16384 + 9, 4),          # + a partial stripe (generic tail per object)
     (32, list(range(8, 40)), 2 * 131072 + 64 * 512, 3),   # whole tiles + a stream of groups
+    (32, [r for r in range(40) if r % 5], 65536, 5),      # syndrome-kernel survivors, objects under one tile
+    (16, list(range(4, 20)), 16384, 7),                    # the same at k = 16
 ])
 def test_fast_restore_object_stream(ec, k, nodes, size, count):
     """Batches of small objects on the bit-sliced runtime-coefficient restore
@@ -326,6 +328,7 @@ def test_restore_path_selection(ec):
     assert _path(32, list(range(8, 40)), 2 * 2048 * 32 + 2) in (2, 3)
     assert _path(5, list(range(5)), L) == 1
     assert _path(32, list(range(32, 64)), 2 * 1024 + 2) == 2       # live shape: 64 KiB objects, stream mode
+    assert _path(32, [r for r in range(40) if r % 5], 2 * 1024 + 2) == 2  # (32, 40) survivors under one tile
 
 
 def test_restore_device_batched(ec):

@@ -267,7 +267,9 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_
   uint64_t per_obj = 0, fast_total = 0;       // fast stripes: per object (whole tiles) / stream
   SynRestoreArgs sa{};
   uint32_t syn_n = 0;
-  const bool syn = cb == 2 && !cells && plan_restore_syn(k, nodes, sa, &syn_n);
+  // (objects under one tile go to the bit-sliced kernel's stream mode below,
+  // whatever the survivor set, as vds_ec_restore16_path reports)
+  const bool syn = cb == 2 && !cells && F >= kTileStripes && plan_restore_syn(k, nodes, sa, &syn_n);
   if (syn) {
     const uint64_t tiles = F / kTileStripes;
     const uint64_t total = tiles * count;

@@ -358,6 +358,9 @@ __device__ __forceinline__ void store_rep(const Plane16 &acc, uint8_t *rep, cons
 #ifndef VDS_ENC_PASS32  // k = 32, n = 40, whole tiles (C4)
 #define VDS_ENC_PASS32 5  // A/B (256 objects, 2 rounds): 2 -> 1266, 3 -> 1335, 4 -> 1311, 5 -> 1396 GiB/s; no spills at 256 VGPRs
 #endif
+#ifndef VDS_ENC_PASS64  // k = 32, n = 64 (the live production shape)
+#define VDS_ENC_PASS64 3
+#endif
 #ifndef VDS_ENC_PASS16  // the same for k = 16 (A/B with the non-temporal, prioritised stores, 512
 #define VDS_ENC_PASS16 5  // objects, 2 rounds: 1 -> 1740, 2 -> 1825, 3 -> 1867, 5 -> 1914 GiB/s encode;
 #endif                    // 5 at k = 32 spills)
@@ -411,7 +414,10 @@ __device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const Fa
 template <int K, int N, int RPW, int WV, int W, bool ST, int S0 = 0>
 __device__ __forceinline__ void encode_wave_group(const uint32_t *set_planes, const FastEncodeArgs &a, TilePos tp,
                                                   int lane, const BitMasks &bm) {
-  constexpr int kPass = K == 16 ? VDS_ENC_PASS16 : (K == 32 && N == 40 && !ST) ? VDS_ENC_PASS32 : VDS_ENC_PASS;
+  constexpr int kPass = K == 16                     ? VDS_ENC_PASS16
+                        : (K == 32 && N == 40 && !ST) ? VDS_ENC_PASS32
+                        : (K == 32 && N == 64)        ? VDS_ENC_PASS64
+                                                      : VDS_ENC_PASS;
   constexpr int PR = kPass < RPW ? kPass : RPW;
   if constexpr (S0 < RPW) {
     encode_pass<K, N, RPW, WV, W, S0, PR, ST>(set_planes, a, tp, lane, bm);

@@ -348,6 +348,10 @@ __device__ __forceinline__ void store_rep(const Plane16 &acc, uint8_t *rep, cons
     store_replica_groups<STREAM>(acc, rep, a, tp, lane, bm);
 }
 
+#ifndef VDS_ENC_CONTIG
+#define VDS_ENC_CONTIG 0  // A/B: contiguous ranges measured slower (encode 1923 -> 1814 GiB/s)
+#endif
+
 #ifndef VDS_ENC_PRIO  // wave priority while a pass issues its stores (A/B; 0 = off)
 #define VDS_ENC_PRIO 2  // A/B (512 objects, 2 rounds): encode 1881-1895 -> 1917-1918 GiB/s
 #endif
@@ -517,9 +521,17 @@ void k_encode_bs(FastEncodeArgs a) {
     else
       encode_load<K>(P, a, t, tset, tp);
   };
+#if VDS_ENC_CONTIG  // A/B: one contiguous range of tiles per workgroup
+  const uint32_t t_per = (a.total_tiles + gridDim.x - 1) / gridDim.x;
+  uint32_t tile = blockIdx.x * t_per;
+  const uint32_t t_end = tile + t_per < a.total_tiles ? tile + t_per : a.total_tiles;
+  const uint32_t t_step = 1;
+#else
   uint32_t tile = blockIdx.x;
-  if (tile < a.total_tiles) load(tile);
-  for (; tile < a.total_tiles; tile += gridDim.x) {
+  const uint32_t t_end = a.total_tiles, t_step = gridDim.x;
+#endif
+  if (tile < t_end) load(tile);
+  for (; tile < t_end; tile += t_step) {
     // ---- transpose to planes and publish in LDS: cell 4p+2g+h, bit b = R[g][16h + (b^8)]
     uint32_t R[2][32];
     if constexpr (kLoad16) {
@@ -545,8 +557,8 @@ void k_encode_bs(FastEncodeArgs a) {
     }
     __syncthreads();
     // ---- prefetch the next tile while this one is evaluated (software pipeline)
-    const uint32_t next = tile + gridDim.x;
-    if (next < a.total_tiles) load(next);
+    const uint32_t next = tile + t_step;
+    if (next < t_end) load(next);
     // ---- evaluate this wave's replicas and store
     encode_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
     __syncthreads();
@@ -835,6 +847,10 @@ __device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t 
 #define VDS_SYN_LATE 1
 #endif
 
+#ifndef VDS_SYN_CONTIG  // 1: each workgroup restores one contiguous range of tiles (A/B)
+#define VDS_SYN_CONTIG 0  // A/B: contiguous ranges measured slower (repair 1572 -> 1460 GiB/s)
+#endif
+
 #ifndef VDS_SYN_PRIO  // wave priority while issuing the survivor loads and the copy-out stores (A/B; 0 = off)
 #define VDS_SYN_PRIO 0  // A/B: 2 measured the same as 0 (repair 1598-1602 vs 1604-1606)
 #endif
@@ -994,8 +1010,18 @@ void k_restore_syn(SynRestoreArgs a) {
   // The next tile's survivors, or zeros past the last tile: both paths define
   // Q, so the values consumed by this tile's stage 1 die there instead of
   // staying live (as loop-carried state) through the programs until the load
+  // tiles of this workgroup: strided over the grid, or (VDS_SYN_CONTIG) one
+  // contiguous range per workgroup
+#if VDS_SYN_CONTIG
+  const uint32_t t_per = (a.total_tiles + gridDim.x - 1) / gridDim.x;
+  const uint32_t t_begin = blockIdx.x * t_per;
+  const uint32_t t_end = t_begin + t_per < a.total_tiles ? t_begin + t_per : a.total_tiles;
+  const uint32_t t_step = 1;
+#else
+  const uint32_t t_begin = blockIdx.x, t_end = a.total_tiles, t_step = gridDim.x;
+#endif
   auto prefetch = [&](uint32_t t) {
-    if (t < a.total_tiles) {
+    if (t < t_end) {
       if constexpr (VDS_SYN_PRIO > 0) __builtin_amdgcn_s_setprio(VDS_SYN_PRIO);
       load(t);
       if constexpr (VDS_SYN_PRIO > 0) __builtin_amdgcn_s_setprio(0);
@@ -1016,8 +1042,8 @@ void k_restore_syn(SynRestoreArgs a) {
   // VDS_SYN_LATE 2: issued inside the output staging, once the first word
   // group's cells are dead (no spills of loop-carried state around them)
   constexpr bool kStageLoad = kLateLoad && VDS_SYN_LATE == 2;
-  if (blockIdx.x < a.total_tiles) load(blockIdx.x);
-  for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+  if (t_begin < t_end) load(t_begin);
+  for (uint32_t tile = t_begin; tile < t_end; tile += t_step) {
     const uint32_t o = tile / a.tiles_per_obj;
     const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
@@ -1058,7 +1084,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #else
       P::syndrome(kSynSameCode ? 1 : wave, L, t.p);
 #endif
-      if (!kLateLoad) prefetch(tile + gridDim.x);
+      if (!kLateLoad) prefetch(tile + t_step);
       st.mark(2);
       // M <= 4: all products before the barrier (their walk overlaps the
       // slower waves' syndromes); M = 8: four at a time after it (eight
@@ -1114,7 +1140,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #else
       P::syndrome(kSynSameCode ? 1 : wave, L, syn);
 #endif
-      prefetch(tile + gridDim.x);
+      prefetch(tile + t_step);
       __syncthreads();  // every wave is done reading the zeroed erased planes
 #pragma unroll
       for (int r = 0; r < S::kSynRows; r += 4) {
@@ -1179,7 +1205,7 @@ void k_restore_syn(SynRestoreArgs a) {
       for (int r = 0; r < 16 * S::kCells; ++r) cells[r] = lane * r;
 #elif VDS_SYN_GM
       syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
-      if (kLateLoad && !kStageLoad) prefetch(tile + gridDim.x);
+      if (kLateLoad && !kStageLoad) prefetch(tile + t_step);
 #else
       P::interp(kSynSameCode ? 1 : wave, L, cells);
 #endif
@@ -1258,7 +1284,7 @@ void k_restore_syn(SynRestoreArgs a) {
             *(__attribute__((address_space(3))) uint32_t *)(w0 + (slot >> 3) * (32768 + 512) + (slot & 7) * 64) =
                 rows[pi];
           }
-          if (kStageLoad && g == 0) prefetch(tile + gridDim.x);
+          if (kStageLoad && g == 0) prefetch(tile + t_step);
         }
         st.mark(15);
         __syncthreads();

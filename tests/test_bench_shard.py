@@ -59,3 +59,24 @@ def test_gloo_world2_sharding_and_max():
     assert own0 == [0, 2, 4] and own1 == [1, 3, 5]          # object o -> rank o % 2, disjoint
     assert got0 == got1 == [2.0, 10.0, 5.0]                  # element-wise MAX over ranks
     assert n0 == n1 == 3                                     # both ranks run the minimum count
+
+
+def test_parent_builds_before_ranks_start(monkeypatch):
+    """bench.py --gpus N builds the library once in the parent (no GPU
+    touched) before torchrun starts the ranks, so the ranks find it fresh."""
+    import bench
+    from vds_amd import build as vbuild
+    seen = {}
+
+    def fake_relaunch(args):
+        seen["stale_at_launch"] = vbuild._stale(vbuild.LIB)
+        seen["gpus"] = args.gpus
+        return 0
+
+    monkeypatch.setattr(bench, "relaunch_with_torchrun", fake_relaunch)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 0
+    assert seen == {"stale_at_launch": False, "gpus": 2}

@@ -4,6 +4,7 @@
 // SIMD.  Sizes the instruction budget of the XOR-program generator.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 
 enum Op { XOR2, BITOP3_V, BITOP3_S, BFI, PERM, PERM_V, LSHL, BITOP3_LIT, ALIGNBIT, DPP, AND_LIT, LSHL_OR };
 
@@ -70,8 +71,15 @@ static void run(const char *name, int waves_per_cu) {
   (void)hipFree(out);
 }
 
-int main() {
-  for (int w : {8, 16}) {
+int main(int argc, char **argv) {
+  // waves per CU to sweep (default 8 and 16 = 2 and 4 waves per SIMD)
+  int ws[8] = {8, 16}, nw = 2;
+  if (argc > 1) {
+    nw = 0;
+    for (int i = 1; i < argc && nw < 8; ++i) ws[nw++] = atoi(argv[i]);
+  }
+  for (int wi = 0; wi < nw; ++wi) {
+    const int w = ws[wi];
     run<XOR2>("xor2", w);
     run<BITOP3_V>("bitop3_v", w);
     run<BITOP3_S>("bitop3_s", w);

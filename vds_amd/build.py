@@ -1,21 +1,33 @@
 """Build libvds_ec.so (HIP kernels + C ABI) in-tree for gfx950.
 
-Used by __graft_entry__.build() and the tests.  The .so lands next to this
-file so it travels to the GPU box with the repository snapshot.
+Used by __graft_entry__.build(), bench.py and the tests.  The .so lands next
+to this file so it travels to the GPU box with the repository snapshot.
+
+Safe to call from several processes at once (bench.py's torchrun ranks, the
+test runner): builds are serialised by an fcntl lock, each build compiles
+into a private temporary directory, and the library is swapped in with one
+atomic rename; a process that waited for the lock re-checks staleness and
+returns the library the other process built.
 """
 from __future__ import annotations
 
+import concurrent.futures as cf
+import fcntl
 import os
 import shutil
 import subprocess
 import sys
+import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvds_ec.so")
-SOURCES = ["ec_kernels.hip", "sha256.hip", "vds_ec_api.cpp"]
-HEADERS = ["bitslice.hpp", "gf_common.hpp", "ec_internal.hpp"]
+LOCK = os.path.join(HERE, ".build.lock")
+# one translation unit per kernel family, compiled in parallel
+SOURCES = ["ec_generic.hip", "ec_encode.hip", "ec_restore_bs.hip", "ec_restore_syn.hip", "sha256.hip",
+           "vds_ec_api.cpp"]
+HEADERS = ["bitslice.hpp", "gf_common.hpp", "ec_internal.hpp", "ec_device.hpp"]
 ARCH = os.environ.get("VDS_EC_ARCH", "gfx950")
 
 
@@ -26,42 +38,67 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: cannot build libvds_ec.so")
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
+def _deps() -> list[str]:
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "vds_ec.h")]
     gen = os.path.join(CSRC, "generated")
     if os.path.isdir(gen):
-        deps += [os.path.join(gen, f) for f in os.listdir(gen)]
-    return any(os.path.getmtime(d) > t for d in deps)
+        deps += [os.path.join(gen, f) for f in sorted(os.listdir(gen))]
+    return deps
+
+
+def _stale(lib: str) -> bool:
+    if not os.path.exists(lib):
+        return True
+    t = os.path.getmtime(lib)
+    return any(os.path.getmtime(d) > t for d in _deps())
+
+
+def compile_cmd(src: str, obj: str, defines: tuple[str, ...] = ()) -> list[str]:
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-c", *defines,
+           "-I", os.path.join(ROOT, "include"), os.path.join(CSRC, src), "-o", obj]
+    if src.endswith(".cpp"):
+        cmd[1:1] = ["-x", "hip"]
+    return cmd
+
+
+def _compile_all(tmp: str, defines: tuple[str, ...], verbose: bool) -> list[str]:
+    jobs = []
+    for src in SOURCES:
+        obj = os.path.join(tmp, src.rsplit(".", 1)[0] + ".o")
+        cmd = compile_cmd(src, obj, defines)
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        jobs.append((cmd, obj))
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 1), 8))
+    with cf.ThreadPoolExecutor(workers) as ex:
+        futs = [ex.submit(subprocess.run, cmd, check=True) for cmd, _ in jobs]
+        for f in futs:
+            f.result()
+    return [obj for _, obj in jobs]
 
 
 def build(force: bool = False, verbose: bool = False, out: str | None = None,
           defines: tuple[str, ...] = ()) -> str:
     """Build the library (default: in-tree libvds_ec.so, rebuilt when stale).
-    `out` + `defines` build a variant (e.g. -DVDS_SYN_PREFETCH=0) for A/B
+    `out` + `defines` build a variant (e.g. -DVDS_DIAG_STAMPS=1) for A/B
     measurements; the variant is loaded with VDS_EC_LIB=<path>."""
     lib = out or LIB
-    if out is None and not force and not _stale():
+    if out is None and not force and not _stale(lib):
         return LIB
-    objs = []
-    for src in SOURCES:
-        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + (".variant.o" if out else ".o"))
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-c", *defines,
-               "-I", os.path.join(ROOT, "include"), os.path.join(CSRC, src), "-o", obj]
-        if src.endswith(".cpp"):
-            cmd[1:1] = ["-x", "hip"]
-        if verbose:
-            print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
-        objs.append(obj)
-    tmp = lib + ".tmp"
-    subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs +
-                   ["-lpthread"], check=True)
-    os.replace(tmp, lib)
-    for o in objs:
-        os.remove(o)
+    os.makedirs(os.path.dirname(os.path.abspath(lib)), exist_ok=True)
+    with open(LOCK, "a+") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if out is None and not force and not _stale(lib):
+                return LIB  # built by another process while this one waited
+            with tempfile.TemporaryDirectory(prefix="vds_build_", dir=HERE) as tmp:
+                objs = _compile_all(tmp, defines, verbose)
+                tmp_lib = os.path.join(tmp, "lib.so")
+                subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp_lib] + objs +
+                               ["-lpthread"], check=True)
+                os.replace(tmp_lib, lib)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
     return lib
 
 

@@ -1,0 +1,86 @@
+// ec_device.hpp -- device-side helpers shared by the kernel translation units
+// (ec_generic.hip, ec_encode.hip, ec_restore_bs.hip, ec_restore_syn.hip).
+// Internal to libvds_ec.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <cstdlib>
+
+#include "bitslice.hpp"
+#include "ec_internal.hpp"
+
+namespace vds_ec {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const volatile u32x4 lds_u32x4;
+typedef __attribute__((address_space(3))) volatile u32x4 lds_v4;
+typedef __attribute__((address_space(3))) char lds_char;
+
+// Streaming (non-temporal) global accesses of the data path, by bit:
+// 1 = encode replica stores, 2 = encode object loads, 4 = restore survivor
+// loads, 8 = restore / regenerate stores.  Every byte is read or written
+// exactly once, so nothing is lost by not keeping it in L2.  Only whole-line
+// wave accesses use them: k_restore_bs's 4-byte strided stores and loads ran
+// 3.4x slower non-temporal (live shape repair 212 -> 79 GiB/s).  Same-box A/B
+// (512 x 64 MiB, 3 rounds): none 840, {1,4,8} 859, all four 856 GiB/s.
+constexpr int kNonTemporal = 1 | 4 | 8;
+
+template <int BIT, class T>
+__device__ __forceinline__ T g_ld(const void *p) {
+  if constexpr ((kNonTemporal & BIT) != 0) return __builtin_nontemporal_load(reinterpret_cast<const T *>(p));
+  else return *reinterpret_cast<const T *>(p);
+}
+template <int BIT, class T>
+__device__ __forceinline__ void g_st(void *p, T v) {
+  if constexpr ((kNonTemporal & BIT) != 0) __builtin_nontemporal_store(v, reinterpret_cast<T *>(p));
+  else *reinterpret_cast<T *>(p) = v;
+}
+
+// The 16 planes of one cell from LDS as four ds_read_b128.  A volatile
+// 128-bit load through an LDS (address_space(3)) pointer keeps the compiler
+// from splitting the reads into ds_read2_b32 / ds_read_b64, which
+// bank-conflict at the encode's padding.
+__device__ __forceinline__ Plane16 lds_planes(const uint32_t *p) {
+  Plane16 x;
+  lds_u32x4 *q = (lds_u32x4 *)(p);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const u32x4 v = q[m];
+    x.p[4 * m + 0] = v.x;
+    x.p[4 * m + 1] = v.y;
+    x.p[4 * m + 2] = v.z;
+    x.p[4 * m + 3] = v.w;
+  }
+  return x;
+}
+
+// ------------------------------------------------------------ host helpers
+
+// Study override of a fast kernel's grid (workgroups), read once per launcher:
+// VDS_EC_ENC_GRID / VDS_EC_SYN_GRID (0 or unset = the default sizing).
+inline uint32_t grid_override(const char *name) {
+  const char *v = std::getenv(name);
+  return v ? (uint32_t)std::strtoul(v, nullptr, 10) : 0u;
+}
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):
+// the attribute is per device, and the multi-GPU host batches launch from one
+// thread per device concurrently.
+template <class Kernel>
+hipError_t ensure_lds_attr(Kernel *k, int bytes) {
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> done[kMaxDev];  // 0 = not yet, 1 = set
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev >= 0 && dev < kMaxDev && done[dev].load(std::memory_order_acquire)) return hipSuccess;
+  e = hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess && dev >= 0 && dev < kMaxDev) done[dev].store(1, std::memory_order_release);
+  return e;
+}
+
+}  // namespace vds_ec

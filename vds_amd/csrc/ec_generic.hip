@@ -1,0 +1,220 @@
+// ec_generic.hip -- the any-shape kernels of the object-chunk erasure codec.
+//
+// One lane per output cell with the carry-less field multiply: any k, any
+// replica ids, 8- or 16-bit cells.  They handle the tails of the bit-sliced
+// kernels (partial tiles, the last partial stripe, trailers) and every shape
+// those are not instantiated for (e.g. chunk_storage's 800-of-1000 ids, the
+// uint8_t template, the cell-array test paths).  Plus the synthetic-object
+// generator used by bench.py and the tests.
+#include "ec_device.hpp"
+
+namespace vds_ec {
+
+template <int CB>
+__device__ __forceinline__ uint32_t gf_mul_cell(uint32_t a, uint32_t b) {
+  if constexpr (CB == 2)
+    return gf16_mul(a, b);
+  else
+    return gf8_mul(a, b);
+}
+
+// Cell j of stripe t of an object, zero beyond `size` (chunk.h:254-260).
+template <int CB>
+__device__ __forceinline__ uint32_t read_cell(const uint8_t *obj, uint64_t size, uint64_t t, uint32_t j,
+                                              uint32_t k, bool native) {
+  const uint64_t pos = (t * k + j) * CB;
+  if constexpr (CB == 1) {
+    return pos < size ? obj[pos] : 0u;
+  } else {
+    if (native) {  // cell arrays: whole native uint16 cells (chunk.h:213-221)
+      return pos + 1 < size ? (uint32_t)(obj[pos] | (obj[pos + 1] << 8)) : 0u;
+    }
+    uint32_t hi = pos < size ? obj[pos] : 0u;
+    uint32_t lo = pos + 1 < size ? obj[pos + 1] : 0u;
+    return (hi << 8) | lo;
+  }
+}
+
+template <int CB>
+__global__ void k_encode_generic(GenericEncodeArgs a) {
+  const uint64_t per_rep = a.t_count + (a.write_trailer ? 1 : 0);
+  const uint64_t total = per_rep * a.nrep * (uint64_t)a.count;
+  const bool native = (a.flags & 0x2u) != 0;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t ti = idx % per_rep;
+    const uint64_t rest = idx / per_rep;
+    const uint32_t i = (uint32_t)(rest % a.nrep);
+    const uint32_t o = (uint32_t)(rest / a.nrep);
+    uint8_t *out = a.outs[i] + (uint64_t)o * a.out_stride;
+    if (ti == a.t_count) {
+      // trailer BE16(size % (k*cell)) after the T cells (chunk.h:273-275)
+      const uint64_t pad = a.size % ((uint64_t)a.k * CB);
+      out[a.stripes * CB] = (uint8_t)(pad >> 8);
+      out[a.stripes * CB + 1] = (uint8_t)(pad & 0xFF);
+      continue;
+    }
+    const uint64_t t = a.t_begin + ti;
+    const uint8_t *obj = a.in + (uint64_t)o * a.in_stride;
+    const uint32_t node = a.nodes[i];
+    uint32_t acc = 0;
+    for (int32_t j = (int32_t)a.k - 1; j >= 0; --j)  // Horner: sum_j node^j x_j
+      acc = gf_mul_cell<CB>(acc, node) ^ read_cell<CB>(obj, a.size, t, (uint32_t)j, a.k, native);
+    if constexpr (CB == 2) {
+      if (native) {
+        out[2 * t] = (uint8_t)(acc & 0xFF);
+        out[2 * t + 1] = (uint8_t)(acc >> 8);
+      } else {
+        out[2 * t] = (uint8_t)(acc >> 8);  // binary_serialize.cpp:18-22
+        out[2 * t + 1] = (uint8_t)(acc & 0xFF);
+      }
+    } else {
+      out[t] = (uint8_t)acc;
+    }
+  }
+}
+
+template <int CB>
+__global__ void k_restore_generic(GenericRestoreArgs a) {
+  const uint64_t per_obj = a.t_count * a.k;
+  const uint64_t total = per_obj * a.count;
+  const bool native = (a.flags & 0x2u) != 0;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t o = (uint32_t)(idx / per_obj);
+    const uint64_t r = idx % per_obj;
+    const uint64_t t = a.t_begin + r / a.k;
+    const uint32_t m = (uint32_t)(r % a.k);
+    const uint64_t pos = (t * a.k + m) * CB;
+    if (pos >= a.out_len) continue;
+    uint32_t acc = 0;
+    const uint64_t row = (uint64_t)m * a.k;
+    for (uint32_t j = 0; j < a.k; ++j) {
+      const uint8_t *base = a.chunk_pitch ? a.chunk_base + (uint64_t)j * a.chunk_pitch
+                                          : (a.chunk_table ? a.chunk_table[j] : a.chunk_ptr[j]);
+      const uint8_t *c = base + (uint64_t)o * a.chunk_stride + t * CB;
+      const uint64_t e = row + j;
+      const uint32_t coef = a.matrix_dev ? a.matrix_dev[e] : (a.matrix_inline[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+      uint32_t cell;
+      if constexpr (CB == 2)
+        cell = native ? (uint32_t)(c[0] | (c[1] << 8)) : (uint32_t)((c[0] << 8) | c[1]);
+      else
+        cell = c[0];
+      acc ^= gf_mul_cell<CB>(coef, cell);
+    }
+    uint8_t *out = a.out + (uint64_t)o * a.out_stride;
+    if constexpr (CB == 2) {
+      const uint8_t b0 = native ? (uint8_t)(acc & 0xFF) : (uint8_t)(acc >> 8);
+      const uint8_t b1 = native ? (uint8_t)(acc >> 8) : (uint8_t)(acc & 0xFF);
+      out[pos] = b0;
+      if (pos + 1 < a.out_len) out[pos + 1] = b1;  // trimmed to E bytes (chunk.h:437-439)
+    } else {
+      out[pos] = (uint8_t)acc;
+    }
+  }
+}
+
+template <int CB>
+__global__ void k_regen_generic(RegenArgs a) {
+  const uint64_t per = a.t_count + 1;  // cells + the trailer
+  const uint64_t total = per * a.nt * (uint64_t)a.count;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t ti = idx % per;
+    const uint64_t rest = idx / per;
+    const uint32_t i = (uint32_t)(rest % a.nt);
+    const uint32_t o = (uint32_t)(rest / a.nt);
+    uint8_t *out = a.outs[i] + (uint64_t)o * a.out_stride;
+    auto chunk = [&](uint32_t j) {
+      return (a.chunk_table ? a.chunk_table[j] : a.chunk_ptr[j]) + (uint64_t)o * a.chunk_stride;
+    };
+    if (ti == a.t_count) {  // trailer BE16(size % (k*cell)), identical in every replica (chunk.h:273-275)
+      const uint8_t *c0 = chunk(0);
+      out[a.T * CB] = c0[a.T * CB];
+      out[a.T * CB + 1] = c0[a.T * CB + 1];
+      continue;
+    }
+    const uint64_t t = a.t_begin + ti;
+    uint32_t acc = 0;
+    for (uint32_t j = 0; j < a.k; ++j) {
+      const uint64_t e = (uint64_t)i * a.k + j;
+      const uint32_t coef = a.coef_dev ? a.coef_dev[e] : (a.coef_inline[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+      const uint8_t *c = chunk(j) + t * CB;
+      const uint32_t cell = CB == 2 ? (uint32_t)((c[0] << 8) | c[1]) : (uint32_t)c[0];
+      acc ^= gf_mul_cell<CB>(coef, cell);
+    }
+    if constexpr (CB == 2) {
+      out[2 * t] = (uint8_t)(acc >> 8);  // binary_serialize.cpp:18-22
+      out[2 * t + 1] = (uint8_t)(acc & 0xFF);
+    } else {
+      out[t] = (uint8_t)acc;
+    }
+  }
+}
+
+// ============================================================== synthetic data
+
+__global__ void k_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed) {
+  const uint64_t words = (size + 7) / 8;
+  for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < words;
+       w += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t z = seed + (w + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    if (8 * w + 8 <= size) {
+      *reinterpret_cast<uint64_t *>(dst + 8 * w) = z;
+    } else {
+      for (uint64_t b = 0; 8 * w + b < size; ++b) dst[8 * w + b] = (uint8_t)(z >> (8 * b));
+    }
+  }
+}
+
+static int grid_for(uint64_t work, int block) {
+  uint64_t g = (work + block - 1) / block;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s) {
+  const uint64_t work = (a.t_count + (a.write_trailer ? 1 : 0)) * a.nrep * (uint64_t)a.count;
+  if (work == 0) return hipSuccess;
+  const int grid = grid_for(work, 256);
+  if (a.cell_bytes == 2)
+    hipLaunchKernelGGL(k_encode_generic<2>, dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_encode_generic<1>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s) {
+  const uint64_t work = a.t_count * a.k * (uint64_t)a.count;
+  if (work == 0) return hipSuccess;
+  const int grid = grid_for(work, 256);
+  if (a.cell_bytes == 2)
+    hipLaunchKernelGGL(k_restore_generic<2>, dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_restore_generic<1>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_regen_generic(const RegenArgs &a, hipStream_t s) {
+  const uint64_t work = (a.t_count + 1) * a.nt * (uint64_t)a.count;
+  if (work == 0) return hipSuccess;
+  const int grid = grid_for(work, 256);
+  if (a.cell_bytes == 2)
+    hipLaunchKernelGGL(k_regen_generic<2>, dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_regen_generic<1>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed, hipStream_t s) {
+  if (size == 0) return hipSuccess;
+  const int grid = grid_for((size + 7) / 8, 256);
+  hipLaunchKernelGGL(k_fill_splitmix, dim3(grid), dim3(256), 0, s, dst, size, seed);
+  return hipGetLastError();
+}
+
+}  // namespace vds_ec

@@ -1,5 +1,5 @@
 // ec_internal.hpp -- launch interface between the C ABI (vds_ec_api.cpp) and
-// the kernels (ec_kernels.hip).  Internal to libvds_ec.so.
+// the kernels (ec_generic.hip, ec_encode.hip, ec_restore_bs.hip, ec_restore_syn.hip).  Internal to libvds_ec.so.
 #pragma once
 
 #include <hip/hip_runtime_api.h>

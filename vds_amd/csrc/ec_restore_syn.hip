@@ -1,0 +1,527 @@
+// ec_restore_syn.hip -- k_restore_syn<K,N>: restore of an object from any K
+// of its N replicas without a per-pattern K x K inverse
+// (chunk_restore<uint16_t>::restore, chunk.h:290-444; instantiated for
+// (16, 20) and (32, 40), the BASELINE configs).
+//
+// With M = N - K erased points E, per 2048-stripe tile:
+//   1. syndromes S_j = sum_a v_a a^j c_a over all N points (erased = 0): a
+//      fixed map, generated XOR programs (tools/xorgen/gen_restore.cpp);
+//   2. recovery c_E = W_E^{-1} S -- the only runtime arithmetic, M x M;
+//   3. interpolation from the fixed points 0..K-1 (one additive-FFT level +
+//      generated half-size programs + an XOR-only expansion);
+//   4. big-endian stores through an LDS staging of the tile.
+// REGEN stops after step 2 and writes the recovered points as replica bytes:
+// the fused repair of sync_process.cpp:313-335 (decode + re-encode).
+#include "ec_device.hpp"
+
+namespace vds_ec {
+
+template <int K, int N, int WV> struct RestorePrograms;
+#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#include "generated/restore_16_20_w4.inc"
+#include "generated/restore_32_40_w8.inc"
+#undef VDS_SCHED_FENCE
+
+// k_restore_syn<K, N, WV>: one 2048-stripe tile per workgroup of WV waves.
+// Two such workgroups share a CU (k = 16); their phases drift apart, so one
+// workgroup's barrier waits and memory phases overlap the other's VALU.  (Two
+// tiles per 8-wave workgroup, which keeps the two waves of a SIMD in the same
+// phase, measured slower: repair 1597 -> 1478-1486 GiB/s at 512 objects.)
+template <int K, int N, int WV>
+struct SynShape {
+  static constexpr int kWaves = WV;
+  static constexpr int kThreads = 64 * WV;
+  static constexpr int kM = N - K;
+  static constexpr int kLoadPer = K / WV;          // survivors loaded per wave
+  using P = RestorePrograms<K, N, WV>;
+  static constexpr int kSynRows = P::kSynRows;     // syndrome bit-rows per wave
+  static constexpr int kCells = P::kIntRows / 16;  // object cells per wave
+  // group-major LDS: plane p = 16 point + bit lives in group p / 4; the four
+  // planes of a group are one 16-byte word per lane, so every access is a
+  // conflict-free ds_{read,write}_b128 (byte (p/4)*1024 + lane*16 + 4*(p%4))
+  static constexpr int kLdsBytes = N * 16 * 64 * 4;
+  static constexpr int kWavesPerSimd = (160 * 1024 / kLdsBytes) * WV / 4;
+  static_assert(K % WV == 0 && kM <= WV, "survivor loads and erased slots must map onto waves");
+  static_assert(kSynRows == 16 && kM == WV, "scatter recovery needs one whole syndrome per wave");
+  static_assert(kCells == 2 || kCells == 4, "row split must be b128 / word-group aligned");
+  static_assert(kLdsBytes <= 160 * 1024, "LDS");
+};
+
+// Diagnostic build (VDS_DIAG_STAMPS=1, timing only): every wave of
+// k_restore_syn accumulates s_memtime deltas per phase of its tiles into
+// g_syn_stamps[block][wave][phase] (read with vds_ec_diag_stamps; phases in
+// tools/syn_stamps.py).  The marks wait for outstanding scalar and LDS
+// operations and the compiler may move VALU work across them: read the
+// barrier waits, not the exact split of neighbouring phases.  Off: the marks
+// compile to nothing.  tests/test_build.py compile-checks this build.
+#ifndef VDS_DIAG_STAMPS
+#define VDS_DIAG_STAMPS 0
+#endif
+#if VDS_DIAG_STAMPS
+constexpr int kStampPhases = 20;
+constexpr int kStampSlots = 4096 * 4 * kStampPhases;
+__device__ unsigned long long g_syn_stamps[kStampSlots];
+struct Stamps {
+  uint64_t prev, acc[kStampPhases];
+  __device__ __forceinline__ void init() {
+    prev = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < kStampPhases; ++i) acc[i] = 0;
+  }
+  __device__ __forceinline__ void mark(int i) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    acc[i] += now - prev;
+    prev = now;
+  }
+  __device__ __forceinline__ void flush(int slot, int lane) {
+    if (lane == 0 && slot < 4096 * 4)
+      for (int i = 0; i < kStampPhases; ++i) g_syn_stamps[slot * kStampPhases + i] = acc[i];
+  }
+};
+#else
+struct Stamps {
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void flush(int, int) {}
+};
+#endif
+
+// Group g of the plane-major LDS as seen by one lane.  ds_read_b128 carries a
+// 16-bit immediate offset, so groups past 64 KiB (points >= 16) are addressed
+// from a second base register; the base is laundered through an empty asm so
+// the compiler does not fold it back into one address register per group.
+struct SynLds {
+  lds_char *base;
+  uint32_t lo;   // 16 * lane
+  uint32_t hi;   // 16 * lane + 64 KiB (opaque)
+  uint32_t hi2;  // 16 * lane + 128 KiB (opaque; points 32.. of k = 32)
+  // A compile-time group is an immediate offset (< 64 KiB) from one of the
+  // three bases, so no per-group address register stays live; a runtime
+  // group costs one address add.
+  __device__ __forceinline__ lds_char *at(int g) const {
+    if (__builtin_constant_p(g)) {
+      if (g < 64) return base + lo + g * 1024;
+      if (g < 128) return base + hi + (g - 64) * 1024;
+      return base + hi2 + (g - 128) * 1024;
+    }
+    return base + lo + g * 1024;
+  }
+  __device__ __forceinline__ u32x4 operator()(int g) const { return *(lds_v4 *)at(g); }
+  __device__ __forceinline__ void put(int g, u32x4 v) const { *(lds_v4 *)at(g) = v; }
+};
+
+__device__ __forceinline__ void syn_put_point(const SynLds &L, int pt, const uint32_t (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) L.put(4 * pt + g, u32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]});
+}
+
+__device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const u32x4 x = L(4 * pt + g);
+    v[4 * g] = x[0];
+    v[4 * g + 1] = x[1];
+    v[4 * g + 2] = x[2];
+    v[4 * g + 3] = x[3];
+  }
+}
+
+// Interpolation from the fixed points F = {0..K-1} by one level of the
+// additive FFT (Gao-Mateer).  F is the GF(2)-span of 1, x, x^2, x^3 (, x^4),
+// so with G = {0, 2, .., K-2} and s(X) = X^2 + X (which maps g and g+1 to the
+// same point):
+//   P(X) = P0(s(X)) + X P1(s(X)),  deg P0, P1 < K/2,
+//   P1(s(g)) = c_g + c_{g+1},  P0(s(g)) = c_g + g P1(s(g)).
+// Stage A forms those K/2 value pairs in place (Q0 -> slot g, Q1 -> slot g+1),
+// stage B interpolates P0 and P1 on D = s(G) with generated XOR programs
+// (RestorePrograms::interpB), and stage C expands (X^2+X)^i = X^i (X+1)^i,
+// whose coefficients are binomials mod 2, so it is XORs only.  About 60% of
+// the XORs of the direct 16-point program (1375 vs 1280 GiB/s).
+template <int W, int NP, int Q = 0>
+__device__ __forceinline__ void syn_gm_stage_a(const SynLds &L) {
+  if constexpr (Q < NP) {
+    constexpr int i = NP * W + Q;  // the pair (g, g + 1) = (2 i, 2 i + 1)
+    Plane16 c0, c1;
+    syn_get_point(L, 2 * i, c0.p);
+    syn_get_point(L, 2 * i + 1, c1.p);
+    const Plane16 q1 = plane_xor(c0, c1);
+    const Plane16 q0 = plane_horner_rows<(uint32_t)(2 * i)>(q1, c0);
+    syn_put_point(L, 2 * i, q0.p);
+    syn_put_point(L, 2 * i + 1, q1.p);
+    syn_gm_stage_a<W, NP, Q + 1>(L);
+  }
+}
+
+// Output cell k = sum of P0_i with C(i, k - i) odd and of P1_i with
+// C(i, k - 1 - i) odd (Lucas: C(i, m) is odd iff the bits of m are a subset of
+// those of i).  P0_i sits in LDS slot i, P1_i in slot K/2 + i.
+template <int K, int W, int NC>
+__device__ __forceinline__ void syn_gm_stage_c(const SynLds &L, uint32_t (&cells)[16 * NC]) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int k = NC * W + c;
+    uint32_t acc[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) acc[b] = 0u;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const int i = t % (K / 2);
+      const int m = t < K / 2 ? k - i : k - 1 - i;
+      if (m >= 0 && m <= i && (m & ~i) == 0) {
+        uint32_t v[16];
+        syn_get_point(L, t, v);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) acc[b] ^= v[b];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 16; ++b) cells[16 * c + b] = acc[b];
+  }
+}
+
+template <int K, int N, int WV, int W>
+__device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
+  static_assert((K == 16 && WV == 4) || (K == 32 && WV == 8),
+                "the one-level interpolation is laid out for k = 16 and k = 32");
+  using P = RestorePrograms<K, N, WV>;
+  constexpr int kPairs = (K / 2) / WV;           // stage-A pairs per wave
+  constexpr int kHalfCells = P::kHalfRows / 16;  // stage-B cells per wave
+  constexpr int kParts = WV / 2;                 // waves per half-size polynomial
+  if constexpr (W < WV) {
+    if (wave != W) return syn_interp_gm<K, N, WV, W + 1>(wave, L, cells, st);
+    syn_gm_stage_a<W, kPairs>(L);
+    st.mark(7);
+    __syncthreads();
+    st.mark(8);
+    uint32_t half[P::kHalfRows];
+    P::interpB(W, L, half);
+    st.mark(9);
+    __syncthreads();  // every wave has read its Q values
+    st.mark(10);
+    // P0 (W < kParts) or P1 cells kHalfCells (W % kParts) + c -> slot (K/2) (W / kParts) + ..
+#pragma unroll
+    for (int c = 0; c < kHalfCells; ++c) {
+      uint32_t v[16];
+#pragma unroll
+      for (int b = 0; b < 16; ++b) v[b] = half[16 * c + b];
+      syn_put_point(L, (K / 2) * (W / kParts) + kHalfCells * (W % kParts) + c, v);
+    }
+    st.mark(11);
+    __syncthreads();
+    st.mark(12);
+    syn_gm_stage_c<K, W, K / WV>(L, cells);
+    st.mark(13);
+  }
+}
+
+// Restore of an object from any K of its N replicas without a per-pattern
+// K x K inverse (tools/xorgen/gen_restore.cpp).  Per tile, wave w:
+//  1. loads survivors kLoadPer*w.. into their points' planes (waves < M also
+//     zero one erased point);
+//  2. computes syndrome S_w over all N points (erased points read as zero)
+//     and scatters its share of every recovered point into the erased slots;
+//  3. interpolates cells kCells*w.. from the fixed points 0..K-1 and stores
+//     them big-endian.
+// Tiles are strided over the grid (one contiguous range of tiles per
+// workgroup measured slower: repair 1572 -> 1460 GiB/s).
+template <int K, int N, int WV, bool REGEN>
+__global__ __launch_bounds__((SynShape<K, N, WV>::kThreads), (SynShape<K, N, WV>::kWavesPerSimd))
+void k_restore_syn(SynRestoreArgs a) {
+  using S = SynShape<K, N, WV>;
+  using P = typename S::P;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const BitMasks bm = bit_masks();
+  SynLds L;
+  L.base = (lds_char *)lds;
+  L.lo = 16u * lane;
+  L.hi = 16u * lane + 65536u;
+  asm volatile("" : "+v"(L.hi));
+  if constexpr (N * 16 > 128) {
+    L.hi2 = 16u * lane + 131072u;
+    asm volatile("" : "+v"(L.hi2));
+  } else {
+    L.hi2 = L.hi;
+  }
+  const int my_erased = wave < S::kM ? a.erased[wave] : 0;
+
+  // survivor staging: the next tile's loads are issued after the syndrome
+  // programs (k = 32: after the interpolation, see kLateLoad) and land while
+  // the rest of this tile runs
+  u32x4 Q[S::kLoadPer][4];
+  auto load = [&](uint32_t t) {
+    const uint32_t ob = t / a.tiles_per_obj;
+    const uint64_t st0 = (uint64_t)(t % a.tiles_per_obj) * kTileStripes;
+#pragma unroll
+    for (int s = 0; s < S::kLoadPer; ++s) {
+      const uint8_t *src = a.chunks[wave * S::kLoadPer + s] + (uint64_t)ob * a.chunk_stride + 2 * st0 + 16 * lane;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Q[s][q] = g_ld<4, u32x4>(src + 1024 * q);
+    }
+  };
+  // The next tile's survivors, or zeros past the last tile: both paths define
+  // Q, so the values consumed by this tile's stage 1 die there instead of
+  // staying live (as loop-carried state) through the programs until the load
+  // (k = 32 spilled 203 VGPRs that way: 1.6x / 1.4x the algorithmic traffic).
+  auto prefetch = [&](uint32_t t) {
+    if (t < a.total_tiles) {
+      load(t);
+    } else {
+#pragma unroll
+      for (int s = 0; s < S::kLoadPer; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Q[s][q] = u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  Stamps st;
+  st.init();
+  // k = 32 (one 160 KiB workgroup per CU): the prefetched survivors would be
+  // live across the syndrome and stage-B programs, which then spill; they are
+  // issued after the interpolation instead and land under the staging and
+  // stores (REGEN has no interpolation and keeps the early issue)
+  constexpr bool kLateLoad = K == 32 && !REGEN;
+  const uint32_t t_step = gridDim.x;
+  prefetch(blockIdx.x);
+  for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += t_step) {
+    const uint32_t o = tile / a.tiles_per_obj;
+    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
+    // ---- 1. survivors -> planes of their points; waves < M zero one erased point
+    {
+      if (wave < S::kM) {
+        const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) L.put(4 * my_erased + g, z);
+      }
+#pragma unroll
+      for (int s = 0; s < S::kLoadPer; ++s) {
+        uint32_t W[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) W[4 * q + d] = Q[s][q][d];
+        transpose16x2(W, bm);  // W[x] = plane of cell bit x^8
+        uint32_t Pl[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) Pl[b] = W[b ^ 8];
+        syn_put_point(L, a.point[wave * S::kLoadPer + s], Pl);
+      }
+    }
+    st.mark(0);
+    __syncthreads();
+    st.mark(1);
+    // ---- 2. wave j holds syndrome S_j whole and scatters its share of every
+    // recovered point, c_e[m] += R[m][j] S_j, into the erased slots (zero since
+    // stage 1) with LDS XOR atomics: T = x^b S_j walks the coefficient bits
+    // once for all M products, and no wave has to gather the syndromes (two
+    // barriers and a park/reload of the syndromes fewer than a gather:
+    // 1384 -> 1525 GiB/s)
+    {
+      Plane16 t;
+      P::syndrome(wave, L, t.p);
+      if (!kLateLoad) prefetch(tile + t_step);
+      st.mark(2);
+      // M <= 4: all products before the barrier (their walk overlaps the
+      // slower waves' syndromes); M = 8: four at a time after it (eight
+      // accumulators would not fit beside the prefetched survivors)
+      constexpr int kMC = S::kM <= 4 ? S::kM : 4;
+      if constexpr (kMC < S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
+#pragma unroll
+      for (int m0 = 0; m0 < S::kM; m0 += kMC) {
+        Plane16 ce[kMC];
+#pragma unroll
+        for (int m = 0; m < kMC; ++m) ce[m] = plane_zero();
+        Plane16 t_copy;  // several chunks walk from the same syndrome
+        Plane16 &tt = kMC < S::kM ? (t_copy = t, t_copy) : t;
+#pragma unroll
+        for (int b = 0; b < 16; b += 2) {
+          const Plane16 t1 = plane_mulx(tt);
+#pragma unroll
+          for (int m = 0; m < kMC; ++m) {
+            const uint32_t two = (a.solve_sel[m0 + m][b >> 2] >> (8 * (b & 3) + wave)) & 0x101u;
+            if (two == 1u)
+              ce[m] = plane_xor(ce[m], tt);
+            else if (two == 0x100u)
+              ce[m] = plane_xor(ce[m], t1);
+            else if (two == 0x101u)
+              ce[m] = plane_xor3(ce[m], tt, t1);
+          }
+          if (b < 14) tt = plane_mulx(t1);
+        }
+        st.mark(3);
+        if constexpr (kMC == S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
+        st.mark(4);
+#pragma unroll
+        for (int m = 0; m < kMC; ++m) {
+          __attribute__((address_space(3))) uint64_t *dst =
+              (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * a.erased[m0 + m]);
+#pragma unroll
+          for (int h = 0; h < 8; ++h)
+            __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1),
+                                   (uint64_t)ce[m].p[2 * h] | ((uint64_t)ce[m].p[2 * h + 1] << 32), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+    st.mark(5);
+    __syncthreads();
+    st.mark(6);
+    if constexpr (REGEN) {
+      // ---- 3'. regenerate: the recovered point e_w IS replica e_w's cells
+      // (P(e_w) stripe by stripe).  Undo the stage-1 transpose and store it as
+      // big-endian cells, one 1 KiB store per wave-instruction; no
+      // interpolation (fused "decode + re-encode" of sync_process.cpp:313-335).
+      if (wave < S::kM && a.regen[wave] != nullptr) {
+        uint32_t Pl[16], W[16];
+        syn_get_point(L, my_erased, Pl);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) W[b ^ 8] = Pl[b];
+        transpose16x2(W, bm);  // self-inverse: back to the loaded word layout
+        uint8_t *dst = a.regen[wave] + (uint64_t)o * a.regen_stride + 2 * stripe0 + 16 * lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          g_st<8>(dst + 1024 * q, u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]});
+      }
+      __syncthreads();  // every wave is done with this tile's planes
+      continue;
+    }
+    // ---- 3. fixed interpolation from points 0..K-1, then big-endian stores
+    {
+      uint32_t cells[16 * S::kCells];
+      syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
+      if (kLateLoad) prefetch(tile + t_step);
+      uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
+      constexpr int kGroups = S::kCells / 2;  // word groups (2 cells) per wave
+      if constexpr (K == 16) {
+        // Stage the tile's output in LDS (the planes are dead once every wave
+        // has interpolated), stripe-major with 16 bytes of padding after every
+        // 16 stripes: the copy-out is 16 contiguous bytes per lane, so every
+        // HBM write is a whole 1 KiB wave-instruction (no partial lines).  One
+        // word group at a time keeps 32, not 64, transposed rows live.
+        static_assert(2048 * 32 + 128 * 16 <= S::kLdsBytes, "staging layout is for 32-byte stripes");
+        __syncthreads();
+        st.mark(14);
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) {
+          uint32_t rows[32];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int jb = 0; jb < 16; ++jb) rows[16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
+          transpose32(rows, bm);
+          // slot 8q+e is stripe st = 8 lane + 512 q + e at byte st*32 + (st/16)*16,
+          // i.e. a per-lane base plus a compile-time offset
+          lds_char *w0 = L.base + 256u * lane + 16u * (lane >> 1) + 4u * (kGroups * wave + g);
+#pragma unroll
+          for (int slot = 0; slot < 32; ++slot) {
+            const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+            *(__attribute__((address_space(3))) uint32_t *)(w0 + (slot >> 3) * (16384 + 512) + (slot & 7) * 32) =
+                rows[pi];
+          }
+        }
+        st.mark(15);
+        __syncthreads();
+        st.mark(16);
+        // 16-byte chunk c = 64 (kChunks wave + i) + lane of the tile: stripe c/2, half c%2
+        constexpr int kChunks = 64 / WV;  // 1 KiB pieces of the tile each wave writes
+        const lds_char *r0 =
+            L.base + 1056u * kChunks * wave + 32u * (lane >> 1) + 16u * (lane >> 5) + 16u * (lane & 1);
+        uint8_t *g0 = dst + stripe0 * (2 * K) + 1024u * kChunks * wave + 16u * lane;
+#pragma unroll
+        for (int i = 0; i < kChunks; ++i) {
+          const u32x4 v = *(lds_v4 *)(r0 + 1056 * i);
+          g_st<8>(g0 + 1024 * i, v);
+        }
+        st.mark(17);
+      } else {
+        // k = 32: stage as for k = 16 with 64-byte stripes and 8 bytes of
+        // padding after every 8 stripes: stripe st, word w at st*64 + (st/8)*8
+        // + 4w; the copy-out reads 16 bytes per lane as two 8-byte halves.
+        static_assert(K == 32 && S::kCells == 4 && 2048 * 64 + 256 * 8 <= S::kLdsBytes,
+                      "staging layout is for 64-byte stripes");
+        __syncthreads();
+        st.mark(14);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          uint32_t rows[32];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int jb = 0; jb < 16; ++jb) rows[16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
+          transpose32(rows, bm);
+          // slot 8q+e is stripe st = 8 lane + 512 q + e: byte 512 lane + 8 lane
+          // + q (32768 + 512) + 64 e + 4 (2 wave + g); lanes l and l + 16 of a
+          // 32-lane group share a bank (one word group at a time keeps 32,
+          // not 64, transposed rows live)
+          lds_char *w0 = L.base + 520u * lane + 4u * (2 * wave + g);
+#pragma unroll
+          for (int slot = 0; slot < 32; ++slot) {
+            const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+            *(__attribute__((address_space(3))) uint32_t *)(w0 + (slot >> 3) * (32768 + 512) + (slot & 7) * 64) =
+                rows[pi];
+          }
+        }
+        st.mark(15);
+        __syncthreads();
+        st.mark(16);
+        // 16-byte chunk c = 64 (16 wave + i) + lane of the tile: stripe c/4,
+        // quarter c%4, at 64 (c/4) + 8 (c/32) + 16 (c%4) = r0 + 1040 i (one
+        // per-lane base, compile-time offsets: no hoisted address per i)
+        uint8_t *g0 = dst + stripe0 * (2 * K) + 16384u * wave + 16u * lane;
+        const lds_char *r0 = L.base + 16640u * wave + 64u * (lane >> 2) + 8u * (lane >> 5) + 16u * (lane & 3);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const lds_char *r = r0 + 1040 * i;
+          const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
+          const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
+          g_st<8>(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]});
+        }
+        st.mark(17);
+      }
+    }
+    __syncthreads();
+    st.mark(18);
+  }
+  st.flush(blockIdx.x * WV + wave, lane);
+}
+
+#if VDS_DIAG_STAMPS
+extern "C" int vds_ec_diag_stamps(unsigned long long *host, size_t n) {
+  if (n > (size_t)kStampSlots) n = kStampSlots;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_syn_stamps), n * sizeof(unsigned long long));
+}
+#endif
+
+// =================================================================== launchers
+
+bool has_restore_syn(uint32_t k, uint32_t n) { return (k == 16 && n == 20) || (k == 32 && n == 40); }
+
+const uint16_t *restore_syn_weights(uint32_t k, uint32_t n) {
+  if (k == 16 && n == 20) return &RestorePrograms<16, 20, 4>::kSyndromeW[0][0];
+  if (k == 32 && n == 40) return &RestorePrograms<32, 40, 8>::kSyndromeW[0][0];
+  return nullptr;
+}
+
+template <int K, int N, int WV, bool REGEN>
+static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) {
+  using S = SynShape<K, N, WV>;
+  hipError_t e = ensure_lds_attr(&k_restore_syn<K, N, WV, REGEN>, S::kLdsBytes);
+  if (e != hipSuccess) return e;
+  const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
+  uint32_t grid = 256u * (blocks_per_cu > 0 ? blocks_per_cu : 1);
+  static const uint32_t over = grid_override("VDS_EC_SYN_GRID");
+  if (over) grid = over;
+  if (grid > a.total_tiles) grid = a.total_tiles;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_restore_syn<K, N, WV, REGEN>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen) {
+  if (k == 16 && n == 20)
+    return regen ? launch_restore_syn_kn<16, 20, 4, true>(a, s) : launch_restore_syn_kn<16, 20, 4, false>(a, s);
+  if (k == 32 && n == 40)
+    return regen ? launch_restore_syn_kn<32, 40, 8, true>(a, s) : launch_restore_syn_kn<32, 40, 8, false>(a, s);
+  return hipErrorNotSupported;
+}
+
+}  // namespace vds_ec

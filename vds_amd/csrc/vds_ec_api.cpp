@@ -4,7 +4,7 @@
 // reference's contracts (chunk.h, chunk_storage.cpp), the Vandermonde
 // inverse (the chunk_restore constructor), dispatch between the bit-sliced
 // and generic kernels, host-memory staging and the multi-GPU batch driver.
-// All data-path arithmetic runs in the HIP kernels of ec_kernels.hip; the
+// All data-path arithmetic runs in the HIP kernels (ec_*.hip); the
 // only host arithmetic is on k x k matrices and tables.
 #include "../../include/vds_ec.h"
 

@@ -239,6 +239,30 @@ __device__ __forceinline__ void encode_dispatch(int wave, const uint32_t *set_pl
       encode_wave_group<K, N, RPW, WV, W, ST>(set_planes, a, tp, lane, bm);
     else
       encode_dispatch<K, N, RPW, WV, ST, W + 1>(wave, set_planes, a, tp, lane, bm);
+  } else {
+    // wave < kWaves: no path through the dispatch skips the stores (a
+    // store-free path would make the vmcnt waits at the top of the tile loop
+    // conservative, see the entry of k_encode_bs)
+    __builtin_unreachable();
+  }
+}
+
+// The stores encode_dispatch issues for one tile, with zero planes: see the
+// entry of k_encode_bs for why.
+template <int K, int N, int RPW, int WV, bool ST, int W>
+__device__ __forceinline__ void encode_zero_dispatch(int wave, const FastEncodeArgs &a, TilePos tp, int lane,
+                                                     const BitMasks &bm) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  if constexpr (W < S::kWaves) {
+    if (wave == W) {
+#pragma unroll
+      for (int s = 0; s < RPW; ++s)
+        if (S::kPlan.rep[W][s] >= 0) store_rep<S::kMap, ST>(plane_zero(), a.outs[S::kPlan.rep[W][s]], a, tp, lane, bm);
+    } else {
+      encode_zero_dispatch<K, N, RPW, WV, ST, W + 1>(wave, a, tp, lane, bm);
+    }
+  } else {
+    __builtin_unreachable();
   }
 }
 
@@ -326,7 +350,20 @@ void k_encode_bs(FastEncodeArgs a) {
   // slower: encode 1923 -> 1814 GiB/s)
   uint32_t tile = blockIdx.x;
   const uint32_t t_end = a.total_tiles, t_step = gridDim.x;
-  if (tile < t_end) load(tile);
+  if (tile < t_end) {
+    load(tile);
+    // vmcnt counts loads and stores together and retires them in issue order.
+    // In the loop a tile's replica stores are issued after the next tile's
+    // loads, so the loads can be waited for while the stores drain.  The
+    // compiler's wait insertion merges the loop's entry and back-edge states
+    // by the youngest position of each pending register: at the entry the
+    // loads ARE the youngest ops, so it would wait vmcnt(1) at the top of
+    // every tile -- for all of the previous tile's stores to complete.
+    // Issuing the same stores here (zeros into this wave's replica cells of
+    // its first tile, which that tile overwrites, in order, from the same
+    // wave) makes both states alike.
+    encode_zero_dispatch<K, N, RPW, WV, STREAM, 0>(wave, a, tile_pos(a, tile), lane, bm);
+  }
   for (; tile < t_end; tile += t_step) {
     // ---- transpose to planes and publish in LDS: cell 4p+2g+h, bit b = R[g][16h + (b^8)]
     uint32_t R[2][32];

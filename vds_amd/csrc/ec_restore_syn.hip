@@ -282,6 +282,25 @@ void k_restore_syn(SynRestoreArgs a) {
   constexpr bool kLateLoad = K == 32 && !REGEN;
   const uint32_t t_step = gridDim.x;
   prefetch(blockIdx.x);
+  // vmcnt counts loads and stores together and retires them in issue order.
+  // In the loop, the 16 copy-out stores of a tile are issued after the next
+  // tile's survivor loads, so the loads can be waited for with vmcnt(16 + ..)
+  // while the stores drain.  The compiler's wait insertion merges the loop's
+  // entry and back-edge states by the youngest position of each pending
+  // register: at the entry the prefetched loads ARE the youngest ops, so it
+  // would wait vmcnt(<16) at the top of every tile -- for the previous tile's
+  // stores to complete.  Issuing the same 16 stores here (zeros into this
+  // wave's copy-out chunk of its first tile, which that tile's copy-out
+  // overwrites, in order, from the same wave) makes both states alike.
+  if constexpr (!REGEN) {
+    if (blockIdx.x < a.total_tiles) {
+      const uint32_t t0 = blockIdx.x;
+      uint8_t *g0 = a.out + (uint64_t)(t0 / a.tiles_per_obj) * a.out_stride +
+                    (uint64_t)(t0 % a.tiles_per_obj) * kTileStripes * (2 * K) + 16384u * wave + 16u * lane;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) g_st<8>(g0 + 1024 * i, u32x4{0u, 0u, 0u, 0u});
+    }
+  }
   for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += t_step) {
     const uint32_t o = tile / a.tiles_per_obj;
     const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;

@@ -57,6 +57,7 @@ struct SynShape {
 #ifndef VDS_DIAG_STAMPS
 #define VDS_DIAG_STAMPS 0
 #endif
+
 #if VDS_DIAG_STAMPS
 constexpr int kStampPhases = 20;
 constexpr int kStampSlots = 4096 * 4 * kStampPhases;
@@ -333,7 +334,9 @@ void k_restore_syn(SynRestoreArgs a) {
     // stage 1) with LDS XOR atomics: T = x^b S_j walks the coefficient bits
     // once for all M products, and no wave has to gather the syndromes (two
     // barriers and a park/reload of the syndromes fewer than a gather:
-    // 1384 -> 1525 GiB/s)
+    // 1384 -> 1525 GiB/s).  The wave-uniform branches measured faster than
+    // their alternatives (512 objects): two separate ifs 1562-1563, masked
+    // v_bitop3 with VGPR masks 1520-1534, against 1573-1577 GiB/s.
     {
       Plane16 t;
       P::syndrome(wave, L, t.p);
@@ -412,43 +415,51 @@ void k_restore_syn(SynRestoreArgs a) {
       constexpr int kGroups = S::kCells / 2;  // word groups (2 cells) per wave
       if constexpr (K == 16) {
         // Stage the tile's output in LDS (the planes are dead once every wave
-        // has interpolated), stripe-major with 16 bytes of padding after every
-        // 16 stripes: the copy-out is 16 contiguous bytes per lane, so every
-        // HBM write is a whole 1 KiB wave-instruction (no partial lines).  One
-        // word group at a time keeps 32, not 64, transposed rows live.
-        static_assert(2048 * 32 + 128 * 16 <= S::kLdsBytes, "staging layout is for 32-byte stripes");
-        __syncthreads();
-        st.mark(14);
+        // has interpolated), stripe-major with 8 bytes of padding after every
+        // 8 stripes: stripe st at byte 32 st + 8 (st / 8).  Each lane writes
+        // its wave's 8 bytes (cells 4w..4w+3) of a stripe with one
+        // ds_write_b64; lane l's stripes 8 l + e are 264 bytes apart, so the
+        // 16 lanes of a write group cover all 32 banks once (16-byte padding
+        // after every 16 stripes put 4 lanes on each bank of a ds_write_b32:
+        // 4-way conflicts).  The copy-out reads 16 contiguous bytes per lane
+        // as two 8-byte halves, so every HBM write is a whole 1 KiB
+        // wave-instruction (no partial lines).
+        static_assert(S::kCells == 4, "one ds_write_b64 = the wave's 4 cells of a stripe");
+        static_assert(2048 * 32 + 256 * 8 <= S::kLdsBytes, "staging layout is for 32-byte stripes");
+        uint32_t rows[2][32];
 #pragma unroll
         for (int g = 0; g < kGroups; ++g) {
-          uint32_t rows[32];
 #pragma unroll
           for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int jb = 0; jb < 16; ++jb) rows[16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
-          transpose32(rows, bm);
-          // slot 8q+e is stripe st = 8 lane + 512 q + e at byte st*32 + (st/16)*16,
-          // i.e. a per-lane base plus a compile-time offset
-          lds_char *w0 = L.base + 256u * lane + 16u * (lane >> 1) + 4u * (kGroups * wave + g);
+            for (int jb = 0; jb < 16; ++jb) rows[g][16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
+          transpose32(rows[g], bm);
+        }
+        __syncthreads();
+        st.mark(14);
+        // slot 8q+e is stripe 8 lane + 512 q + e at byte 264 lane + 16896 q +
+        // 32 e: a per-lane base plus a compile-time offset
+        lds_char *w0 = L.base + 264u * lane + 8u * wave;
 #pragma unroll
-          for (int slot = 0; slot < 32; ++slot) {
-            const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
-            *(__attribute__((address_space(3))) uint32_t *)(w0 + (slot >> 3) * (16384 + 512) + (slot & 7) * 32) =
-                rows[pi];
-          }
+        for (int slot = 0; slot < 32; ++slot) {
+          const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+          *(__attribute__((address_space(3))) u32x2 *)(w0 + (slot >> 3) * 16896 + (slot & 7) * 32) =
+              u32x2{rows[0][pi], rows[1][pi]};
         }
         st.mark(15);
         __syncthreads();
         st.mark(16);
-        // 16-byte chunk c = 64 (kChunks wave + i) + lane of the tile: stripe c/2, half c%2
+        // 16-byte chunk c = 64 (kChunks wave + i) + lane of the tile: stripe c/2,
+        // half c%2, at 16 c + 8 (c / 16) = r0 + 1056 i
         constexpr int kChunks = 64 / WV;  // 1 KiB pieces of the tile each wave writes
-        const lds_char *r0 =
-            L.base + 1056u * kChunks * wave + 32u * (lane >> 1) + 16u * (lane >> 5) + 16u * (lane & 1);
+        const lds_char *r0 = L.base + 1056u * kChunks * wave + 16u * lane + 8u * (lane >> 4);
         uint8_t *g0 = dst + stripe0 * (2 * K) + 1024u * kChunks * wave + 16u * lane;
 #pragma unroll
         for (int i = 0; i < kChunks; ++i) {
-          const u32x4 v = *(lds_v4 *)(r0 + 1056 * i);
-          g_st<8>(g0 + 1024 * i, v);
+          const lds_char *r = r0 + 1056 * i;
+          const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
+          const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
+          g_st<8>(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]});
         }
         st.mark(17);
       } else {

@@ -39,6 +39,10 @@ extern "C" {
 #define VDS_EC_ESINGULAR (-4) /* replica ids not distinct: V not invertible   */
 #define VDS_EC_ERESTORE (-5)  /* "Fatal error at chunk_restore::restore"      */
 #define VDS_EC_EHIP (-6)      /* HIP runtime error during a launch / copy     */
+/* base64::to_bytes failures (encoding.cpp:181-247), by the reference's text: */
+#define VDS_EC_EB64_LENGTH (-7)  /* "Non-Valid base64!" (length % 4 != 0)      */
+#define VDS_EC_EB64_PADDING (-8) /* "Invalid Padding in Base 64!"              */
+#define VDS_EC_EB64_CHAR (-9)    /* "Non-Valid Character in Base 64!"          */
 
 /* ----------------------------------------------------------------- flags */
 /* write_padding = false in chunk_generator::write (chunk.h:79,273-278):
@@ -181,6 +185,36 @@ int vds_ec_encode16_hash_host(uint16_t k, const uint16_t *replicas, uint32_t n, 
  * NUL-terminated paths of VDS_EC_PATH_BYTES bytes each.                     */
 #define VDS_EC_PATH_BYTES 48
 int vds_ec_replica_paths(const uint8_t *digests, uint32_t count, char *out);
+
+/* ------------------------------------------- upload path
+ * The live upload: websocket "upload" with a base64 body
+ * (websocket_api.cpp:141-155) -> server_api::upload_data (server_api.cpp:12-30:
+ * data hash = SHA-256 of the body) -> _client::save_temp
+ * (dht_network_client.cpp:62-107: replicas 0..n-1 written, each named by its
+ * SHA-256 and kept as <root>/tmp/<tmp name>) -> the JSON answer
+ * (websocket_api.cpp:467-485).  Host code except vds_ec_save_temp16_host,
+ * which runs the encode and every hash on the current device.              */
+/* base64::to_bytes with its quirks (see vds_ec_wire.cpp); *out_len receives
+ * vds_ec_base64_decoded_size(in, len) bytes written to out.                 */
+size_t vds_ec_base64_decoded_size(const char *in, size_t len);
+int vds_ec_base64_decode(const char *in, size_t len, uint8_t *out, size_t *out_len);
+/* base64::from_bytes; out == NULL queries the length (excluding the NUL). */
+int vds_ec_base64_encode(const uint8_t *in, size_t len, char *out, size_t cap, size_t *out_len);
+/* save_temp's tmp-file names: base64 of each digest with '+' -> '#' and
+ * '/' -> '_' (dht_network_client.cpp:91-95), NUL-terminated, 45 bytes each. */
+#define VDS_EC_NAME_BYTES 45
+int vds_ec_tmp_names(const uint8_t *digests, uint32_t count, char *out);
+/* The "upload" answer {"id":..,"result":{"replicas":[..],"hash":..,
+ * "replica_size":..}} exactly as json_writer serialises it; out == NULL
+ * queries the length (excluding the NUL).                                   */
+int vds_ec_upload_response_json(int id, const uint8_t *replica_digests, uint32_t n, const uint8_t *data_digest,
+                                 uint32_t replica_size, char *out, size_t cap, size_t *out_len);
+/* save_temp + upload_data's hashing on the device: replicas 0..n-1 of the
+ * body (host, size bytes) into outs (n host buffers of vds_ec_replica_size
+ * bytes), their SHA-256 names into replica_digests (n*32 host bytes), the
+ * body's SHA-256 into data_digest (32 host bytes).                          */
+int vds_ec_save_temp16_host(uint16_t k, uint32_t n, const uint8_t *data, uint64_t size, uint8_t *const *outs,
+                            uint8_t *replica_digests, uint8_t *data_digest, uint32_t *replica_size);
 
 /* ----------------------------------------------------------------- utilities */
 /* Fill `size` device bytes at dst with the splitmix64 stream of `seed`

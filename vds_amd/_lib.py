@@ -19,6 +19,9 @@ ENOMEM = -3
 ESINGULAR = -4
 ERESTORE = -5
 EHIP = -6
+EB64_LENGTH = -7
+EB64_PADDING = -8
+EB64_CHAR = -9
 
 F_NO_TRAILER = 0x1
 F_CELLS = 0x2
@@ -66,6 +69,14 @@ SIGNATURES = {
     "vds_ec_fill_splitmix_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]),
     "vds_ec_encode16_path": (C.c_int, [C.c_uint16, u16p, C.c_uint32, C.c_uint64]),
     "vds_ec_restore16_path": (C.c_int, [C.c_uint16, u16p, C.c_uint64]),
+    "vds_ec_base64_decoded_size": (C.c_size_t, [C.c_char_p, C.c_size_t]),
+    "vds_ec_base64_decode": (C.c_int, [C.c_char_p, C.c_size_t, C.c_void_p, C.POINTER(C.c_size_t)]),
+    "vds_ec_base64_encode": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "vds_ec_tmp_names": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    "vds_ec_upload_response_json": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p,
+                                              C.c_size_t, C.POINTER(C.c_size_t)]),
+    "vds_ec_save_temp16_host": (C.c_int, [C.c_uint16, C.c_uint32, C.c_void_p, C.c_uint64, vpp, C.c_void_p,
+                                          C.c_void_p, C.POINTER(C.c_uint32)]),
 }
 
 _lib = None

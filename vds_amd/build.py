@@ -26,7 +26,7 @@ LIB = os.path.join(HERE, "libvds_ec.so")
 LOCK = os.path.join(HERE, ".build.lock")
 # one translation unit per kernel family, compiled in parallel
 SOURCES = ["ec_generic.hip", "ec_encode.hip", "ec_restore_bs.hip", "ec_restore_syn.hip", "sha256.hip",
-           "vds_ec_api.cpp"]
+           "vds_ec_api.cpp", "vds_ec_wire.cpp"]
 HEADERS = ["bitslice.hpp", "gf_common.hpp", "ec_internal.hpp", "ec_device.hpp"]
 ARCH = os.environ.get("VDS_EC_ARCH", "gfx950")
 

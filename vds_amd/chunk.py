@@ -308,6 +308,79 @@ def replica_storage_paths(digests) -> list:
     return [bytes(out[48 * i:48 * i + 46]).decode() for i in range(count)]
 
 
+# ------------------------------------------------- upload path (wire formats)
+
+def base64_decode(text) -> bytes:
+    """base64::to_bytes (encoding.cpp:181-247), reference quirks included;
+    raises VdsEcError with the reference's message on malformed input."""
+    raw = text.encode() if isinstance(text, str) else bytes(text)
+    size = _lib.lib().vds_ec_base64_decoded_size(raw, len(raw))
+    out = np.empty(max(1, size), dtype=np.uint8)
+    n = C.c_size_t(0)
+    check(_lib.lib().vds_ec_base64_decode(raw, len(raw), out.ctypes.data, C.byref(n)), "base64_decode")
+    return bytes(out[: n.value])
+
+
+def base64_encode(data) -> str:
+    """base64::from_bytes (encoding.cpp:138-174)."""
+    buf = _u8(data)
+    n = C.c_size_t(0)
+    lib = _lib.lib()
+    check(lib.vds_ec_base64_encode(buf.ctypes.data if buf.size else None, buf.size, None, 0, C.byref(n)))
+    out = C.create_string_buffer(n.value + 1)
+    check(lib.vds_ec_base64_encode(buf.ctypes.data if buf.size else None, buf.size, out, n.value + 1, C.byref(n)))
+    return out.value.decode()
+
+
+def tmp_names(digests) -> list:
+    """save_temp's tmp-file names of replicas (dht_network_client.cpp:91-95)."""
+    d = np.ascontiguousarray(np.frombuffer(b"".join(bytes(x) for x in digests), dtype=np.uint8))
+    count = d.size // 32
+    out = np.zeros(45 * max(count, 1), dtype=np.uint8)
+    check(_lib.lib().vds_ec_tmp_names(d.ctypes.data if count else None, count, out.ctypes.data), "tmp_names")
+    return [bytes(out[45 * i:45 * i + 44]).decode() for i in range(count)]
+
+
+def upload_response_json(req_id: int, replica_digests, data_digest, replica_size: int) -> str:
+    """The websocket answer to "upload" (websocket_api.cpp:120-121, 472-482)."""
+    d = np.ascontiguousarray(np.frombuffer(b"".join(bytes(x) for x in replica_digests), dtype=np.uint8))
+    n = d.size // 32
+    h = np.frombuffer(bytes(data_digest), dtype=np.uint8).copy()
+    ln = C.c_size_t(0)
+    lib = _lib.lib()
+    args = (req_id, d.ctypes.data if n else None, n, h.ctypes.data, replica_size)
+    check(lib.vds_ec_upload_response_json(*args, None, 0, C.byref(ln)))
+    out = C.create_string_buffer(ln.value + 1)
+    check(lib.vds_ec_upload_response_json(*args, out, ln.value + 1, C.byref(ln)))
+    return out.value.decode()
+
+
+def save_temp(k: int, n: int, body):
+    """upload_data + save_temp on the device (server_api.cpp:12-30,
+    dht_network_client.cpp:62-107): replicas 0..n-1 of `body`, their SHA-256
+    names, the body's SHA-256 and the replica size."""
+    buf = _u8(body)
+    L = replica_size(k, buf.size)
+    outs = [np.empty(max(L, 1), dtype=np.uint8) for _ in range(n)]
+    rd = np.empty((max(1, n), 32), dtype=np.uint8)
+    dd = np.empty(32, dtype=np.uint8)
+    rs = C.c_uint32(0)
+    ptrs = (C.c_void_p * max(1, n))(*[o.ctypes.data for o in outs])
+    check(_lib.lib().vds_ec_save_temp16_host(k, n, buf.ctypes.data if buf.size else None, buf.size, ptrs,
+                                             rd.ctypes.data, dd.ctypes.data, C.byref(rs)), "save_temp16_host")
+    return [o[:L] for o in outs], [bytes(x) for x in rd[:n]], bytes(dd), rs.value
+
+
+def upload(req_id: int, body_b64, k: int = 32, n: int = 64):
+    """The live upload end to end: websocket "upload" body (base64) ->
+    replicas, tmp-file names and the JSON answer (MIN_HORCRUX = 32,
+    GENERATE_HORCRUX = 64 by default, dht_network.h:22-25)."""
+    body = base64_decode(body_b64)
+    reps, names, data_hash, rsize = save_temp(k, n, body)
+    return {"replicas": reps, "tmp_names": tmp_names(names), "replica_digests": names, "data_hash": data_hash,
+            "json": upload_response_json(req_id, names, data_hash, rsize)}
+
+
 def fill_splitmix_device(dst, size: int, seed: int, stream=None) -> None:
     ptr = dst.data_ptr() if hasattr(dst, "data_ptr") else int(dst)
     check(_lib.lib().vds_ec_fill_splitmix_device(ptr, size, seed, _stream_ptr(stream)), "fill_splitmix")

@@ -797,6 +797,9 @@ const char *vds_ec_strerror(int status) {
     case VDS_EC_ESINGULAR: return "replica ids are not distinct (singular Vandermonde matrix)";
     case VDS_EC_ERESTORE: return "Fatal error at chunk_restore::restore";
     case VDS_EC_EHIP: return "HIP runtime error";
+    case VDS_EC_EB64_LENGTH: return "Non-Valid base64!";
+    case VDS_EC_EB64_PADDING: return "Invalid Padding in Base 64!";
+    case VDS_EC_EB64_CHAR: return "Non-Valid Character in Base 64!";
     default: return "unknown vds_ec status";
   }
 }
@@ -1171,6 +1174,48 @@ int vds_ec_encode16_hash_host(uint16_t k, const uint16_t *replicas, uint32_t n, 
     if (e != hipSuccess) return hip_status(e);
   }
   e = hipMemcpyAsync(digests, c.d_param, 32ull * n, hipMemcpyDeviceToHost, c.stream);
+  if (e != hipSuccess) return hip_status(e);
+  return hip_status(hipStreamSynchronize(c.stream));
+}
+
+int vds_ec_save_temp16_host(uint16_t k, uint32_t n, const uint8_t *data, uint64_t size, uint8_t *const *outs,
+                            uint8_t *replica_digests, uint8_t *data_digest, uint32_t *replica_size) {
+  if (k == 0 || (n > 0 && (!outs || !replica_digests)) || !data_digest || (size > 0 && !data)) return VDS_EC_EINVAL;
+  int rc = device_ready();
+  if (rc) return rc;
+  const uint64_t L = vds_ec_replica_size(2, k, size, 0);
+  if (replica_size) *replica_size = (uint32_t)L;  // save_temp: replica 0's size (dht_network_client.cpp:81-83)
+  HostCtx *cp = host_ctx();
+  if (!cp) return VDS_EC_ENODEV;
+  HostCtx &c = *cp;
+  rc = c.ensure(size ? size : 1, L * n ? L * n : 1);
+  if (!rc) rc = c.grow(&c.d_param, &c.d_param_cap, 32ull * (n + 1));
+  if (rc) return rc;
+  hipError_t e = hipSuccess;
+  if (size) e = hipMemcpyAsync(c.d_in, data, size, hipMemcpyHostToDevice, c.stream);
+  if (e != hipSuccess) return hip_status(e);
+  // upload_data's hash of the body (server_api.cpp:16)
+  e = launch_sha256(c.d_in, size, size, 1, c.d_param + 32ull * n, c.stream);
+  if (e != hipSuccess) return hip_status(e);
+  if (n) {
+    std::vector<uint16_t> ids(n);
+    std::vector<uint8_t *> douts(n);
+    for (uint32_t i = 0; i < n; ++i) {
+      ids[i] = (uint16_t)i;
+      douts[i] = c.d_out + (uint64_t)i * L;
+    }
+    rc = encode_device(2, k, ids.data(), n, c.d_in, size, size, 1, douts.data(), 0, 0, c.stream);
+    if (rc) return rc;
+    e = launch_sha256(c.d_out, L, L, n, c.d_param, c.stream);  // save_temp's replica names (:79)
+    if (e != hipSuccess) return hip_status(e);
+    for (uint32_t i = 0; i < n; ++i) {
+      e = hipMemcpyAsync(outs[i], douts[i], L, hipMemcpyDeviceToHost, c.stream);
+      if (e != hipSuccess) return hip_status(e);
+    }
+    e = hipMemcpyAsync(replica_digests, c.d_param, 32ull * n, hipMemcpyDeviceToHost, c.stream);
+    if (e != hipSuccess) return hip_status(e);
+  }
+  e = hipMemcpyAsync(data_digest, c.d_param + 32ull * n, 32, hipMemcpyDeviceToHost, c.stream);
   if (e != hipSuccess) return hip_status(e);
   return hip_status(hipStreamSynchronize(c.stream));
 }

@@ -113,7 +113,7 @@ def cpu_baseline(k, n, size, nodes, count):
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
 
 
-def kernel_names(k, n, nodes, size, L):
+def kernel_names(k, n, nodes, size, L, objects):
     """Names of the kernels the C ABI dispatches for this workload."""
     import ctypes as C
     import numpy as np
@@ -121,7 +121,7 @@ def kernel_names(k, n, nodes, size, L):
     ids = np.arange(n, dtype=np.uint16)
     nd = np.asarray(nodes, dtype=np.uint16)
     ep = _lib.lib().vds_ec_encode16_path(k, ids.ctypes.data_as(_lib.u16p), n, C.c_uint64(size))
-    rp = _lib.lib().vds_ec_restore16_path(k, nd.ctypes.data_as(_lib.u16p), C.c_uint64(L))
+    rp = _lib.lib().vds_ec_restore16_path(k, nd.ctypes.data_as(_lib.u16p), C.c_uint64(L), size % (2 * k), objects)
     enc = {2: f"k_encode_bs<{k},{n}>"}.get(ep, "k_encode_generic")
     rep = {3: f"k_restore_syn<{k},{n}>", 2: f"k_restore_bs<{k}>"}.get(rp, "k_restore_generic")
     return enc, rep
@@ -288,7 +288,7 @@ def main():
 
     enc_bytes = objects * (size + n * L)      # S + n*(2*ceil(S/2k)+2)
     rep_bytes = objects * (k * L + size)      # k*L + S
-    enc_name, rep_name = kernel_names(k, n, nodes, size, L)
+    enc_name, rep_name = kernel_names(k, n, nodes, size, L, objects)
     if enc_ms >= rep_ms:
         dom, dom_bytes, dom_ms = enc_name, enc_bytes, enc_ms
     else:

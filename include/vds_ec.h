@@ -15,8 +15,10 @@
  * Any k distinct replicas restore the object (chunk.h:290-444).
  *
  * Memory: *_device entry points take device pointers and enqueue work on the
- * given hipStream_t (NULL = the per-thread default stream) without
- * synchronising.  *_host entry points take host pointers, stage through
+ * given hipStream_t (NULL = the current device's null stream) without
+ * synchronising; parameters too large for the kernel arguments (k > 32
+ * inverses, k > 64 chunk tables) are staged stream-ordered through a pinned
+ * ring (growing it, on first use of a larger size, allocates).  *_host entry points take host pointers, stage through
  * pinned buffers on the current device and return when the result is in host
  * memory.  Every entry point fails with VDS_EC_ENODEV if no GPU is usable --
  * there is no CPU fallback.
@@ -226,10 +228,12 @@ int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void
  * restore (erasure-pattern-independent XOR programs, survivors within
  * 0..k+k/4-1) for the full tiles, 2 = bit-sliced fast path for the full tiles
  * (+ generic tail; objects under one tile whose stripes are whole 512-stripe
- * groups ride it in batches), 1 = generic path only.  VDS_EC_RESTORE_PATH=bs in the
- * environment disables path 3 (for A/B measurements).                       */
+ * groups ride it in batches), 1 = generic path only.  The restore query takes
+ * the trailer's padding and the batch's object count, as
+ * vds_ec_restore16_device does (restore planning is shared with it).
+ * VDS_EC_RESTORE_PATH=bs in the environment disables path 3 (A/B).          */
 int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint64_t size);
-int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size);
+int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size, uint16_t padding, uint32_t count);
 /* 3 = the regenerate rides the syndrome kernel (every target an erased point
  * of a compiled (k, n)) for the full tiles, 2 = the runtime-coefficient
  * bit-sliced kernel (k in {16, 32}, at most k targets, >= 512 full stripes),

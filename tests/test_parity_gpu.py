@@ -250,7 +250,7 @@ def test_fast_restore_tiles_and_tail(ec, k, n):
         for erased in ([0, 1, 2, 3][: n - k], list(range(n - (n - k), n)), list(range(0, n, n // (n - k)))[: n - k]):
             nodes = [r for r in range(n) if r not in erased][:k]
             L = enc.shape[2]
-            assert _lib.lib().vds_ec_restore16_path(k, None, L) == 2
+            assert _lib.lib().vds_ec_restore16_path(k, None, L, size % (2 * k), 1) == 2
             out = torch.zeros(size + 64, dtype=torch.uint8, device="cuda")
             chunk.restore_device(k, nodes, [enc[r, 0].data_ptr() for r in nodes], L, 0, size % (2 * k), 1, out, 0)
             torch.cuda.synchronize()
@@ -258,10 +258,10 @@ def test_fast_restore_tiles_and_tail(ec, k, n):
             assert int(out[size:].sum().item()) == 0  # trimmed to E bytes
 
 
-def _path(k, nodes, L):
+def _path(k, nodes, L, padding=0, count=1):
     from vds_amd import _lib
     arr = np.asarray(nodes, dtype=np.uint16)
-    return _lib.lib().vds_ec_restore16_path(k, arr.ctypes.data_as(_lib.u16p), L)
+    return _lib.lib().vds_ec_restore16_path(k, arr.ctypes.data_as(_lib.u16p), L, padding, count)
 
 
 @pytest.mark.parametrize("k,n", [(16, 20), (32, 40)])
@@ -327,8 +327,16 @@ def test_restore_path_selection(ec):
     assert _path(16, list(range(4, 20)), 2 * 100 + 2) == 1         # no full tile
     assert _path(32, list(range(8, 40)), 2 * 2048 * 32 + 2) in (2, 3)
     assert _path(5, list(range(5)), L) == 1
-    assert _path(32, list(range(32, 64)), 2 * 1024 + 2) == 2       # live shape: 64 KiB objects, stream mode
-    assert _path(32, [r for r in range(40) if r % 5], 2 * 1024 + 2) == 2  # (32, 40) survivors under one tile
+    assert _path(32, list(range(32, 64)), 2 * 1024 + 2, 0, 2) == 2  # live shape: 64 KiB objects, stream mode
+    assert _path(32, list(range(32, 64)), 2 * 1024 + 2, 0, 1) == 1  # ... needs two objects for one tile
+    assert _path(32, [r for r in range(40) if r % 5], 2 * 1024 + 2, 0, 4) == 2  # (32, 40) survivors under one tile
+    # a non-zero trailer padding leaves one stripe fewer whose cells all land
+    # in the output (F = T - 1): the query follows restore_device
+    assert _path(16, list(range(4, 20)), 2 * 2048 + 2, 0) == 3
+    assert _path(16, list(range(4, 20)), 2 * 2048 + 2, 7) == 1
+    assert _path(32, list(range(32, 64)), 2 * 1024 + 2, 5, 64) == 1
+    assert _path(32, list(range(32, 64)), 2 * 1536 + 2, 0, 64) == 2
+    assert _path(32, list(range(32, 64)), 2 * 1536 + 2, 3, 64) == 1
 
 
 def test_restore_device_batched(ec):
@@ -519,3 +527,36 @@ def test_restore_host_batch(ec, k, n):
         c[-2], c[-1] = 0xFF, 0xFF
     with pytest.raises(VdsEcError):
         ec.restore_host_batch(k, [nodes[1]], [bad])
+
+
+def test_large_k_parameters_are_stream_ordered(ec):
+    """k > 32 (the inverse does not fit the kernel arguments) and k > 64 (nor
+    does the chunk table): restore_device and regenerate_device stage them
+    through the stream-ordered parameter ring.  Several calls with different
+    survivor sets are enqueued back to back on one stream with no host sync in
+    between; each must see its own parameters (oracle-checked)."""
+    import torch
+    from vds_amd import chunk
+    rng = np.random.default_rng(77)
+    stream = torch.cuda.Stream()
+    for k, n, size in ((40, 48, 40 * 2 * 37 + 11), (80, 90, 80 * 2 * 9 + 3)):
+        host = O.splitmix(SEED + k, size)
+        t = torch.from_numpy(host.copy()).cuda()
+        reps = dev_encode(torch, k, n, t, size, replicas=list(range(n)))
+        L = reps.shape[2]
+        trials = [sorted(rng.choice(n, k, replace=False).tolist()) for _ in range(6)]
+        outs = [torch.zeros(size + 2 * k, dtype=torch.uint8, device="cuda") for _ in trials]
+        regen_targets = [[r for r in range(n) if r not in nodes][:8] for nodes in trials]
+        regen_outs = [torch.zeros((8, L), dtype=torch.uint8, device="cuda") for _ in trials]
+        torch.cuda.synchronize()
+        with torch.cuda.stream(stream):
+            for nodes, out, tg, ro in zip(trials, outs, regen_targets, regen_outs):
+                chunk.restore_device(k, nodes, [reps[r, 0].data_ptr() for r in nodes], L, 0, size % (2 * k), 1,
+                                     out, 0, stream=stream)
+                chunk.regenerate_device(k, nodes, [reps[r, 0].data_ptr() for r in nodes], L, 0, 1, tg,
+                                        [ro[i].data_ptr() for i in range(len(tg))], L, stream=stream)
+        stream.synchronize()
+        for nodes, out, tg, ro in zip(trials, outs, regen_targets, regen_outs):
+            assert np.array_equal(out[:size].cpu().numpy(), host), (k, nodes)
+            for i, r in enumerate(tg):
+                assert np.array_equal(ro[i].cpu().numpy(), O.encode(k, r, host)), (k, nodes, r)

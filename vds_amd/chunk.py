@@ -221,9 +221,13 @@ class ChunkStorage:
 # --------------------------------------------------------------- device forms
 
 def _stream_ptr(stream) -> int | None:
+    """A hipStream_t for the C ABI: None = torch's current stream; a
+    torch.cuda.Stream or a raw handle otherwise."""
     if stream is None:
         import torch
         return torch.cuda.current_stream().cuda_stream
+    if hasattr(stream, "cuda_stream"):
+        return stream.cuda_stream
     return int(stream)
 
 

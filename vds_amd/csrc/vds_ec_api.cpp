@@ -11,6 +11,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <climits>
+#include <cstdint>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -235,6 +237,137 @@ int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n,
   return VDS_EC_OK;
 }
 
+// ------------------------------------------------ stream-ordered parameters
+// Kernel parameters too large for the kernel arguments (k > 32 inverses, k >
+// 64 chunk tables, regenerate coefficients beyond kInlineCoef) ride a
+// per-device ring of pinned host + device slots, so the *_device entry points
+// enqueue without synchronising.  A slot's bytes are written on the host,
+// copied with hipMemcpyAsync on the caller's stream, and an event recorded
+// after the kernels that read them; a slot is reused only once its event has
+// completed, and hipEventSynchronize blocks only when the ring has wrapped
+// round inside the GPU's queue.  (The round-1 version copied a std::vector
+// on the caller's stack with hipMemcpyAsync and freed a hipMallocAsync
+// buffer in a destructor: the copy could read the vector after it was gone
+// -- the likely cause of that round's fault)  Growing a slot
+// allocates, which synchronises; slots only grow.
+struct ParamSlot {
+  uint8_t *h = nullptr, *d = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+
+struct ParamRing {
+  static constexpr int kSlots = 16;
+  std::mutex mu;
+  ParamSlot slot[kSlots];
+  unsigned next = 0;
+};
+
+ParamRing *param_ring() {
+  static std::mutex m;
+  static std::vector<ParamRing *> rings;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
+  std::lock_guard<std::mutex> g(m);
+  if ((size_t)dev >= rings.size()) rings.resize(dev + 1, nullptr);
+  if (!rings[dev]) rings[dev] = new ParamRing();  // never freed: outlives every caller
+  return rings[dev];
+}
+
+// Stage `bytes` from blob into a device slot on stream s; *dev receives the
+// device address.  Call param_release(slot, s) after the launches reading it.
+hipError_t param_stage(const std::vector<uint8_t> &blob, hipStream_t s, const uint8_t **dev, ParamSlot **out) {
+  ParamRing *r = param_ring();
+  if (!r) return hipErrorNoDevice;
+  std::lock_guard<std::mutex> g(r->mu);
+  ParamSlot &sl = r->slot[r->next++ % ParamRing::kSlots];
+  hipError_t e = hipSuccess;
+  if (sl.pending) {
+    e = hipEventSynchronize(sl.ev);
+    sl.pending = false;
+    if (e != hipSuccess) return e;
+  }
+  if (!sl.ev && (e = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming)) != hipSuccess) return e;
+  if (blob.size() > sl.cap) {
+    if (sl.h) (void)hipHostFree(sl.h);
+    if (sl.d) (void)hipFree(sl.d);
+    sl.h = sl.d = nullptr;
+    sl.cap = 0;
+    if ((e = hipHostMalloc(&sl.h, blob.size(), 0)) != hipSuccess) return e;
+    if ((e = hipMalloc(&sl.d, blob.size())) != hipSuccess) return e;
+    sl.cap = blob.size();
+  }
+  std::memcpy(sl.h, blob.data(), blob.size());
+  if ((e = hipMemcpyAsync(sl.d, sl.h, blob.size(), hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+  *dev = sl.d;
+  *out = &sl;
+  return hipSuccess;
+}
+
+hipError_t param_release(ParamSlot *sl, hipStream_t s) {
+  ParamRing *r = param_ring();
+  if (!r || !sl) return hipSuccess;
+  std::lock_guard<std::mutex> g(r->mu);
+  const hipError_t e = hipEventRecord(sl->ev, s);
+  sl->pending = e == hipSuccess;
+  return e;
+}
+
+template <typename T>
+size_t blob_append(std::vector<uint8_t> &blob, const T *p, size_t n) {
+  const size_t off = (blob.size() + 15) & ~size_t(15);
+  blob.resize(off + sizeof(T) * n);
+  std::memcpy(blob.data() + off, p, sizeof(T) * n);
+  return off;
+}
+
+// ------------------------------------------------------- restore planning
+// Which kernels restore_device runs for these parameters (shared with the
+// vds_ec_restore16_path query, so the two cannot disagree):
+//   3 = k_restore_syn over the whole 2048-stripe tiles of every object,
+//   2 = k_restore_bs over 512-stripe groups (whole tiles per object, or a
+//       stream of tiles across objects when the groups of an object are not
+//       a multiple of 4),
+//   1 = the generic kernel only.
+// F counts the stripes whose k cells all land in the output (out_len / 2k:
+// one fewer than the replica's cells when the trailer's padding is non-zero).
+struct RestorePlan {
+  int path = 1;
+  uint64_t tiles = 0;  // path 3: tiles per object
+  uint64_t gpo = 0;    // path 2: 512-stripe groups per object
+  SynRestoreArgs sa{};
+  uint32_t syn_n = 0;
+};
+
+RestorePlan plan_restore(unsigned cb, uint32_t k, const uint16_t *nodes, uint64_t out_len, uint32_t count,
+                         unsigned flags) {
+  RestorePlan p;
+  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
+  if (cb != 2 || cells || k == 0 || count == 0) return p;
+  const uint64_t F = out_len / (2ull * k);
+  // (objects under one tile go to the bit-sliced kernel's stream mode,
+  // whatever the survivor set)
+  if (F >= kTileStripes && plan_restore_syn(k, nodes, p.sa, &p.syn_n)) {
+    const uint64_t tiles = F / kTileStripes;
+    if (tiles * count <= 0xFFFFFFFFull) {
+      p.path = 3;
+      p.tiles = tiles;
+      return p;
+    }
+  }
+  if (has_restore_fast(k)) {
+    // 512-stripe groups; tiles of 4 groups may straddle objects when 512 | F
+    const uint64_t gpo = F % 512 == 0 ? F / 512 : 4 * (F / kTileStripes);
+    const uint64_t total = gpo * count / 4;
+    if (gpo > 0 && gpo <= 0xFFFFFFFFull && total > 0 && total <= 0xFFFFFFFFull) {
+      p.path = 2;
+      p.gpo = gpo;
+    }
+  }
+  return p;
+}
+
 // --------------------------------------------------------- restore core
 // Optional layout facts the host path knows: chunks contiguous at a pitch,
 // and a device copy of a large inverse already staged.
@@ -251,11 +384,9 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_
   if (count == 0 || out_len == 0) return VDS_EC_OK;
   int rc = device_ready();
   if (rc) return rc;
-  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
   // Every cell of a chunk, the trailer cell included: with a corrupt trailer
   // the reference decodes that row too (chunk.h:421-441).
   const uint64_t cells_per_chunk = chunk_size / cb;
-  (void)cells;
   const uint64_t stripe_bytes = (uint64_t)k * cb;
   uint64_t need = (out_len + stripe_bytes - 1) / stripe_bytes;  // stripes that produce output
   if (need > cells_per_chunk) need = cells_per_chunk;
@@ -265,45 +396,34 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_
   // stream of objects of F full output stripes each); the generic kernel the rest.
   const uint64_t F = out_len / stripe_bytes;  // stripes whose k cells all land in the output
   uint64_t per_obj = 0, fast_total = 0;       // fast stripes: per object (whole tiles) / stream
-  SynRestoreArgs sa{};
-  uint32_t syn_n = 0;
-  // (objects under one tile go to the bit-sliced kernel's stream mode below,
-  // whatever the survivor set, as vds_ec_restore16_path reports)
-  const bool syn = cb == 2 && !cells && F >= kTileStripes && plan_restore_syn(k, nodes, sa, &syn_n);
-  if (syn) {
-    const uint64_t tiles = F / kTileStripes;
-    const uint64_t total = tiles * count;
-    if (tiles > 0 && total <= 0xFFFFFFFFull) {
-      for (uint32_t j = 0; j < k; ++j) sa.chunks[j] = chunks[j];
-      sa.chunk_stride = chunk_stride;
-      sa.out = out;
-      sa.out_stride = out_stride;
-      sa.tiles_per_obj = (uint32_t)tiles;
-      sa.total_tiles = (uint32_t)total;
-      hipError_t e = launch_restore_syn(k, syn_n, sa, s);
-      if (e != hipSuccess) return hip_status(e);
-      per_obj = tiles * kTileStripes;
-    }
-  } else if (cb == 2 && !cells && has_restore_fast(k)) {
-    // 512-stripe groups; tiles of 4 groups may straddle objects when 512 | F
-    const uint64_t gpo = F % 512 == 0 ? F / 512 : 4 * (F / kTileStripes);
-    const uint64_t total = gpo * count / 4;
-    if (gpo > 0 && gpo <= 0xFFFFFFFFull && total > 0 && total <= 0xFFFFFFFFull) {
-      FastRestoreArgs fa{};
-      for (uint32_t j = 0; j < k; ++j) fa.chunks[j] = chunks[j];
-      fa.chunk_stride = chunk_stride;
-      fa.out = out;
-      fa.out_stride = out_stride;
-      fa.groups_per_obj = (uint32_t)gpo;
-      fa.total_tiles = (uint32_t)total;
-      for (uint32_t i = 0; i < k * k; ++i) fa.matrix2[i >> 1] |= uint32_t(matrix[i]) << (16 * (i & 1));
-      hipError_t e = launch_restore_fast(k, fa, s);
-      if (e != hipSuccess) return hip_status(e);
-      if (gpo % 4 == 0)
-        per_obj = 512 * gpo;
-      else
-        fast_total = 512 * 4 * total;
-    }
+  RestorePlan plan = plan_restore(cb, k, nodes, out_len, count, flags);
+  if (plan.path == 3) {
+    SynRestoreArgs &sa = plan.sa;
+    for (uint32_t j = 0; j < k; ++j) sa.chunks[j] = chunks[j];
+    sa.chunk_stride = chunk_stride;
+    sa.out = out;
+    sa.out_stride = out_stride;
+    sa.tiles_per_obj = (uint32_t)plan.tiles;
+    sa.total_tiles = (uint32_t)(plan.tiles * count);
+    hipError_t e = launch_restore_syn(k, plan.syn_n, sa, s);
+    if (e != hipSuccess) return hip_status(e);
+    per_obj = plan.tiles * kTileStripes;
+  } else if (plan.path == 2) {
+    const uint64_t gpo = plan.gpo, total = gpo * count / 4;
+    FastRestoreArgs fa{};
+    for (uint32_t j = 0; j < k; ++j) fa.chunks[j] = chunks[j];
+    fa.chunk_stride = chunk_stride;
+    fa.out = out;
+    fa.out_stride = out_stride;
+    fa.groups_per_obj = (uint32_t)gpo;
+    fa.total_tiles = (uint32_t)total;
+    for (uint32_t i = 0; i < k * k; ++i) fa.matrix2[i >> 1] |= uint32_t(matrix[i]) << (16 * (i & 1));
+    hipError_t e = launch_restore_fast(k, fa, s);
+    if (e != hipSuccess) return hip_status(e);
+    if (gpo % 4 == 0)
+      per_obj = 512 * gpo;
+    else
+      fast_total = 512 * 4 * total;
   }
   // generic remainder: [0, o_full) from per_obj (or F), object o_full from its
   // covered prefix, objects after it from 0
@@ -321,26 +441,28 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_
   for (const Part &pt : parts) any |= pt.cnt > 0 && need > pt.t_begin;
   if (any) {
     GenericRestoreArgs ga{};
-    // Temporaries for parameters that do not fit in the kernel arguments;
-    // freed after a stream sync (only reached for k > 32 or k > 64 chunks).
-    void *tmp_table = nullptr, *tmp_matrix = nullptr;
+    // Parameters that do not fit in the kernel arguments (k > 32 inverse,
+    // k > 64 chunk table) ride the stream-ordered parameter ring.
+    std::vector<uint8_t> blob;
+    size_t off_table = SIZE_MAX, off_matrix = SIZE_MAX;
+    const bool use_table = !layout.pitch && k > (uint32_t)kInlineChunks;
+    if (use_table) off_table = blob_append(blob, chunks, k);
+    if (k <= (uint32_t)kInlineMatrixK) {
+      for (uint32_t i = 0; i < k * k; ++i) ga.matrix_inline[i >> 1] |= uint32_t(matrix[i]) << (16 * (i & 1));
+    } else if (layout.matrix_dev) {
+      ga.matrix_dev = layout.matrix_dev;
+    } else {
+      off_matrix = blob_append(blob, matrix, (size_t)k * k);
+    }
     hipError_t e = hipSuccess;
-    if (!layout.pitch && k > (uint32_t)kInlineChunks) {
-      e = hipMalloc(&tmp_table, sizeof(uint8_t *) * k);
-      if (e == hipSuccess) e = hipMemcpy(tmp_table, chunks, sizeof(uint8_t *) * k, hipMemcpyHostToDevice);
-      ga.chunk_table = static_cast<const uint8_t *const *>(tmp_table);
+    ParamSlot *slot = nullptr;
+    if (!blob.empty()) {
+      const uint8_t *d = nullptr;
+      e = param_stage(blob, s, &d, &slot);
+      if (e == hipSuccess && off_table != SIZE_MAX) ga.chunk_table = reinterpret_cast<const uint8_t *const *>(d + off_table);
+      if (e == hipSuccess && off_matrix != SIZE_MAX) ga.matrix_dev = reinterpret_cast<const uint16_t *>(d + off_matrix);
     }
-    if (e == hipSuccess) {
-      if (k <= (uint32_t)kInlineMatrixK) {
-        for (uint32_t i = 0; i < k * k; ++i) ga.matrix_inline[i >> 1] |= uint32_t(matrix[i]) << (16 * (i & 1));
-      } else if (layout.matrix_dev) {
-        ga.matrix_dev = layout.matrix_dev;
-      } else {
-        e = hipMalloc(&tmp_matrix, sizeof(uint16_t) * (size_t)k * k);
-        if (e == hipSuccess) e = hipMemcpy(tmp_matrix, matrix, sizeof(uint16_t) * (size_t)k * k, hipMemcpyHostToDevice);
-        ga.matrix_dev = static_cast<const uint16_t *>(tmp_matrix);
-      }
-    }
+    const bool tmp_table = use_table;
     for (const Part &pt : parts) {
       if (e != hipSuccess || pt.cnt == 0 || need <= pt.t_begin) continue;
       if (tmp_table && pt.o0) {  // (k > 64: only reached without the fast path, i.e. o0 == 0)
@@ -365,11 +487,9 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_
       ga.out_len = out_len;
       e = launch_restore_generic(ga, s);
     }
-    if (tmp_table || tmp_matrix) {
-      const hipError_t se = hipStreamSynchronize(s);
-      if (e == hipSuccess) e = se;
-      if (tmp_table) (void)hipFree(tmp_table);
-      if (tmp_matrix) (void)hipFree(tmp_matrix);
+    if (slot) {
+      const hipError_t re = param_release(slot, s);
+      if (e == hipSuccess) e = re;
     }
     if (e != hipSuccess) return hip_status(e);
   }
@@ -612,31 +732,33 @@ int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint
       }
     }
   }
-  // generic path: the remaining cells and the trailers, <= 64 targets per launch
-  void *tmp_table = nullptr, *tmp_coef = nullptr;
-  hipError_t e = hipSuccess;
-  if (k > (uint32_t)kInlineChunks) {
-    e = hipMalloc(&tmp_table, sizeof(uint8_t *) * k);
-    if (e == hipSuccess) e = hipMemcpy(tmp_table, chunks, sizeof(uint8_t *) * k, hipMemcpyHostToDevice);
+  // generic path: the remaining cells and the trailers, <= 64 targets per
+  // launch; a k > 64 chunk table and coefficient blocks beyond kInlineCoef
+  // ride the stream-ordered parameter ring (one staged blob for the call)
+  std::vector<uint8_t> blob;
+  const bool tmp_table = k > (uint32_t)kInlineChunks;
+  const size_t off_table = tmp_table ? blob_append(blob, chunks, k) : SIZE_MAX;
+  std::vector<std::vector<uint16_t>> coef_blocks;
+  std::vector<size_t> coef_off;
+  for (uint32_t base = 0; base < nt; base += kMaxLaunchReplicas) {
+    coef_blocks.push_back(coefs(base, std::min<uint32_t>(nt - base, kMaxLaunchReplicas)));
+    const auto &c = coef_blocks.back();
+    coef_off.push_back(c.size() > (size_t)kInlineCoef ? blob_append(blob, c.data(), c.size()) : SIZE_MAX);
   }
-  for (uint32_t base = 0; base < nt && e == hipSuccess; base += kMaxLaunchReplicas) {
+  hipError_t e = hipSuccess;
+  ParamSlot *slot = nullptr;
+  const uint8_t *dparam = nullptr;
+  if (!blob.empty()) e = param_stage(blob, s, &dparam, &slot);
+  for (uint32_t base = 0, bi = 0; base < nt && e == hipSuccess; base += kMaxLaunchReplicas, ++bi) {
     RegenArgs ga{};
     ga.nt = std::min<uint32_t>(nt - base, kMaxLaunchReplicas);
-    if (tmp_table) ga.chunk_table = static_cast<const uint8_t *const *>(tmp_table);
-    const std::vector<uint16_t> coef = coefs(base, ga.nt);
-    if (coef.size() <= (size_t)kInlineCoef) {
+    if (tmp_table) ga.chunk_table = reinterpret_cast<const uint8_t *const *>(dparam + off_table);
+    const std::vector<uint16_t> &coef = coef_blocks[bi];
+    if (coef_off[bi] == SIZE_MAX) {
       for (size_t x = 0; x < coef.size(); ++x) ga.coef_inline[x >> 1] |= uint32_t(coef[x]) << (16 * (x & 1));
     } else {
-      if (tmp_coef) {
-        (void)hipStreamSynchronize(s);
-        (void)hipFree(tmp_coef);
-        tmp_coef = nullptr;
-      }
-      e = hipMalloc(&tmp_coef, sizeof(uint16_t) * coef.size());
-      if (e == hipSuccess) e = hipMemcpy(tmp_coef, coef.data(), sizeof(uint16_t) * coef.size(), hipMemcpyHostToDevice);
-      ga.coef_dev = static_cast<const uint16_t *>(tmp_coef);
+      ga.coef_dev = reinterpret_cast<const uint16_t *>(dparam + coef_off[bi]);
     }
-    if (e != hipSuccess) break;
     ga.chunk_stride = chunk_stride;
     ga.k = k;
     ga.cell_bytes = cb;
@@ -657,11 +779,9 @@ int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint
       e = launch_regen_generic(ga, s);
     }
   }
-  if (tmp_table || tmp_coef) {
-    const hipError_t se = hipStreamSynchronize(s);
-    if (e == hipSuccess) e = se;
-    if (tmp_table) (void)hipFree(tmp_table);
-    if (tmp_coef) (void)hipFree(tmp_coef);
+  if (slot) {
+    const hipError_t re = param_release(slot, s);
+    if (e == hipSuccess) e = re;
   }
   return hip_status(e);
 }
@@ -1297,16 +1417,11 @@ int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint6
   return (contiguous && has_encode_fast(k, n) && fast) ? 2 : 1;
 }
 
-int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size) {
-  const uint64_t T = (k && chunk_size >= 2) ? (chunk_size - 2) / 2 : 0;  // full stripes of an unpadded object
-  const uint64_t tiles = T / kTileStripes;
-  // objects under one tile: stream mode of the bit-sliced kernel when their
-  // stripes are whole 512-stripe groups (batches of >= 2048 / T objects)
-  if (tiles == 0) return (T > 0 && T % 512 == 0 && has_restore_fast(k)) ? 2 : 1;
-  SynRestoreArgs sa{};
-  uint32_t n = 0;
-  if (plan_restore_syn(k, nodes, sa, &n)) return 3;
-  return has_restore_fast(k) ? 2 : 1;
+int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size, uint16_t padding, uint32_t count) {
+  bool ok = true;
+  const uint64_t len = restored_len(2, k, chunk_size, padding, 0, &ok);
+  if (!ok || k == 0) return 1;
+  return plan_restore(2, k, nodes, len, count, 0).path;
 }
 
 }  // extern "C"

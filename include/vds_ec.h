@@ -126,7 +126,28 @@ int vds_ec_regenerate16_device(uint16_t k, const uint16_t *nodes, const uint8_t 
                                uint64_t chunk_stride, uint32_t count, const uint16_t *targets, uint32_t ntargets,
                                uint8_t *const *outs, uint64_t out_stride, void *stream);
 
-/* ---------------------------------------------------------- host entry points
+/* Batched restore / regenerate with a survivor set, size and output PER
+ * OBJECT -- the shape of the download and repair loops (restore_async takes
+ * the first k replicas found for each object, dht_network_client.cpp:851-901;
+ * sync_process repairs object by object, sync_process.cpp:313-335).  Object
+ * o's survivor j (replica id nodes[o*k + j]) is at chunks[o*k + j] (HOST
+ * array of count*k device pointers), chunk_sizes[o] bytes (trailer included);
+ * paddings[o] is its trailer value (the caller has it: the chunks came from
+ * files or sockets).  Restore writes vds_ec_restored_size(2, k,
+ * chunk_sizes[o], paddings[o]) bytes to outs[o].  Regenerate writes replica
+ * targets[o*nt + i] (chunk_sizes[o] bytes, trailer included) to
+ * outs[o*nt + i].  Objects whose survivors lie within the syndrome kernel's
+ * points (k in {16, 32}, ids < k + k/4) share ONE launch; the others take
+ * one launch each.  Every object is validated before anything is enqueued;
+ * nothing synchronises.                                                      */
+int vds_ec_restore16_batch_device(uint16_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
+                                  const uint64_t *chunk_sizes, const uint16_t *paddings, uint8_t *const *outs,
+                                  unsigned flags, void *stream);
+int vds_ec_regenerate16_batch_device(uint16_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
+                                     const uint64_t *chunk_sizes, uint32_t ntargets, const uint16_t *targets,
+                                     uint8_t *const *outs, void *stream);
+
+/* ---------------------------------------------------------- host entry points/* ---------------------------------------------------------- host entry points
  * Same operations on host memory (pinned staging, H2D -> kernel -> D2H on
  * the calling thread's current device).  outs: n host buffers of
  * vds_ec_replica_size(...) bytes.  This is what chunk_generator::write and

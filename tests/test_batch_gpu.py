@@ -1,0 +1,108 @@
+"""Batched restore / regenerate with a survivor set, size and output per
+object (vds_ec_restore16_batch_device / vds_ec_regenerate16_batch_device):
+the download and repair loops' shape (restore_async takes the first k
+replicas found per object, dht_network_client.cpp:851-901; sync_process
+repairs object by object, sync_process.cpp:313-335).  Every object is checked
+against the oracle (chunk.h:402-444 / chunk.h:245-281)."""
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+
+SEED = 0x7664730000000000
+pytestmark = pytest.mark.gpu
+
+
+def _objects(torch, k, n, sizes, seed):
+    """Encode objects of the given sizes (all n replicas, oracle-checked
+    encode path) into separate device buffers: [(host bytes, [n tensors])]."""
+    from vds_amd import chunk
+    out = []
+    for i, size in enumerate(sizes):
+        host = O.splitmix(SEED + seed + i, size)
+        t = torch.from_numpy(host.copy()).cuda() if size else torch.zeros(1, dtype=torch.uint8, device="cuda")
+        L = chunk.replica_size(k, size)
+        reps = [torch.zeros(L, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        chunk.encode_device(k, list(range(n)), t, size, size, 1, [r.data_ptr() for r in reps], L)
+        out.append((host, reps))
+    return out
+
+
+def _first_k_found(rng, k, n_total, lost):
+    """restore_async's choice: the first k replica ids not lost, in order."""
+    gone = set(rng.choice(n_total, lost, replace=False).tolist()) if lost else set()
+    return [r for r in range(n_total) if r not in gone][:k]
+
+
+@pytest.mark.parametrize("k,n_total", [(16, 20), (32, 40), (32, 64)])
+def test_restore_batch_per_object_survivors(gpu, k, n_total):
+    import torch
+    from vds_amd import chunk
+    rng = np.random.default_rng(k * 100 + n_total)
+    tile = 2048 * 2 * k
+    sizes = [0, 1, 2 * k, 2 * k * 7 + 3, tile - 1, tile, tile + 5, 2 * tile + 2 * k * 3 + 1, 65536, 58113,
+             3 * tile + 11] + [int(x) for x in rng.integers(1, 3 * tile, 9)]
+    objs = _objects(torch, k, n_total, sizes, seed=k)
+    nodes, chunks, csz, pads, outs = [], [], [], [], []
+    for (host, reps), size in zip(objs, sizes):
+        lost = int(rng.integers(0, n_total - k + 1))
+        nd = _first_k_found(rng, k, n_total, lost)
+        if rng.random() < 0.3:  # any order of the survivors
+            nd = list(rng.permutation(nd))
+        nodes.append(nd)
+        chunks.append([reps[r].data_ptr() for r in nd])
+        csz.append(reps[0].numel())
+        pads.append(size % (2 * k))
+        outs.append(torch.full((size + 4 * k,), 0xA5, dtype=torch.uint8, device="cuda"))
+    chunk.restore_batch_device(k, nodes, chunks, csz, pads, [o.data_ptr() for o in outs])
+    torch.cuda.synchronize()
+    for (host, reps), size, out, nd in zip(objs, sizes, outs, nodes):
+        got = out.cpu().numpy()
+        ref = O.restore(k, nd, [reps[r].cpu().numpy() for r in nd])
+        assert np.array_equal(got[:size], ref), (size, nd)
+        assert np.array_equal(got[:size], host)
+        assert (got[size:] == 0xA5).all(), size  # nothing written past the object
+
+
+@pytest.mark.parametrize("k,n_total", [(16, 20), (32, 40), (32, 64)])
+def test_regenerate_batch_per_object(gpu, k, n_total):
+    import torch
+    from vds_amd import chunk
+    rng = np.random.default_rng(7 + k + n_total)
+    tile = 2048 * 2 * k
+    sizes = [1, 2 * k * 9 + 1, tile, tile + 2 * k, 2 * tile + 7, 65536] + [int(x) for x in rng.integers(1, 2 * tile, 6)]
+    objs = _objects(torch, k, n_total, sizes, seed=500 + k)
+    nt = 2
+    nodes, chunks, csz, targets, outs = [], [], [], [], []
+    for host, reps in objs:
+        nd = _first_k_found(rng, k, n_total, int(rng.integers(nt, n_total - k + 1)))
+        missing = [r for r in range(n_total) if r not in nd]
+        tg = sorted(rng.choice(missing, nt, replace=False).tolist())
+        nodes.append(nd)
+        chunks.append([reps[r].data_ptr() for r in nd])
+        csz.append(reps[0].numel())
+        targets.append(tg)
+        outs.append([torch.full((reps[0].numel() + 16,), 0x5A, dtype=torch.uint8, device="cuda") for _ in tg])
+    chunk.regenerate_batch_device(k, nodes, chunks, csz, targets, [[o.data_ptr() for o in os_] for os_ in outs])
+    torch.cuda.synchronize()
+    for (host, reps), tg, os_ in zip(objs, targets, outs):
+        L = reps[0].numel()
+        for t, o in zip(tg, os_):
+            got = o.cpu().numpy()
+            assert np.array_equal(got[:L], O.encode(k, t, host)), (host.size, t)
+            assert (got[L:] == 0x5A).all()
+
+
+def test_restore_batch_rejects_bad_objects(gpu):
+    import torch
+    from vds_amd import chunk
+    from vds_amd._lib import VdsEcError, ERESTORE
+    k, n = 16, 20
+    (host, reps), = _objects(torch, k, n, [1000], seed=900)
+    out = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    nd = list(range(k))
+    # a trailer claiming more bytes than the replicas hold: "Fatal error" (chunk.h:443), nothing enqueued
+    with pytest.raises(VdsEcError) as e:
+        chunk.restore_batch_device(k, [nd, nd], [[reps[r].data_ptr() for r in nd]] * 2, [reps[0].numel()] * 2,
+                                   [1000 % 32, 65535], [out.data_ptr()] * 2)
+    assert e.value.status == ERESTORE

@@ -251,6 +251,40 @@ def restore_device(k: int, nodes: Sequence[int], chunks: Sequence[int], chunk_si
                                              out_ptr, out_stride, 0, _stream_ptr(stream)), "restore16_device")
 
 
+def restore_batch_device(k: int, nodes: Sequence[Sequence[int]], chunks: Sequence[Sequence[int]],
+                         chunk_sizes: Sequence[int], paddings: Sequence[int], outs: Sequence[int],
+                         stream=None) -> None:
+    """vds_ec_restore16_batch_device: object o restored from its own survivors
+    nodes[o] at device pointers chunks[o] (chunk_sizes[o] bytes, trailer
+    value paddings[o]) into the device pointer outs[o]."""
+    count = len(nodes)
+    ids = _ids([r for nd in nodes for r in nd], 2)
+    cp = (C.c_void_p * max(1, count * k))(*[int(c) for ch in chunks for c in ch])
+    cs = np.asarray(chunk_sizes, dtype=np.uint64)
+    pd = np.asarray(paddings, dtype=np.uint16)
+    op = (C.c_void_p * max(1, count))(*[int(o) for o in outs])
+    check(_lib.lib().vds_ec_restore16_batch_device(k, count, _idp(ids, 2), cp, cs.ctypes.data_as(_lib.u64p),
+                                                   pd.ctypes.data_as(_lib.u16p), op, 0, _stream_ptr(stream)),
+          "restore16_batch_device")
+
+
+def regenerate_batch_device(k: int, nodes: Sequence[Sequence[int]], chunks: Sequence[Sequence[int]],
+                            chunk_sizes: Sequence[int], targets: Sequence[Sequence[int]],
+                            outs: Sequence[Sequence[int]], stream=None) -> None:
+    """vds_ec_regenerate16_batch_device: replicas targets[o] of object o from
+    its own survivors, into the device pointers outs[o]."""
+    count = len(nodes)
+    nt = len(targets[0]) if count else 0
+    ids = _ids([r for nd in nodes for r in nd], 2)
+    tg = _ids([t for ts in targets for t in ts], 2)
+    cp = (C.c_void_p * max(1, count * k))(*[int(c) for ch in chunks for c in ch])
+    cs = np.asarray(chunk_sizes, dtype=np.uint64)
+    op = (C.c_void_p * max(1, count * nt))(*[int(x) for os_ in outs for x in os_])
+    check(_lib.lib().vds_ec_regenerate16_batch_device(k, count, _idp(ids, 2), cp, cs.ctypes.data_as(_lib.u64p), nt,
+                                                      _idp(tg, 2), op, _stream_ptr(stream)),
+          "regenerate16_batch_device")
+
+
 def regenerate_host(k: int, nodes: Sequence[int], chunks: Sequence, targets: Sequence[int]) -> list:
     """vds_ec_regenerate16_host: replicas `targets` of one object from k
     survivor replicas (host buffers), bytes as restore + re-encode."""

@@ -109,6 +109,10 @@ struct SynRestoreArgs {
   // requested); the interpolation is skipped
   uint8_t *regen[kMaxFastK / 4];
   uint64_t regen_stride;
+  // batch mode (launch_restore_syn_batch): everything per object from tables
+  const struct SynBatchObj *objs;
+  const struct SynBatchPlan *plans;
+  const uint32_t *tile_obj;
 };
 
 constexpr int kInlineCoef = 512;  // regenerate coefficients carried in the kernel arguments
@@ -135,11 +139,32 @@ struct RegenArgs {
   uint64_t out_stride;
 };
 
+// Batched k_restore_syn (per-object survivor sets, sizes and outputs; one
+// launch over every tile of every object).  Device tables, built on the host:
+// objs[o] for each object, plans[p] for each distinct erased set, tile_obj[t]
+// = the object of tile t (an object's tiles are consecutive).
+struct SynBatchObj {
+  const uint8_t *chunks[kMaxFastK];  // survivor j of the object (K used)
+  uint8_t *out;                      // restore: the object's bytes
+  uint8_t *regen[kMaxFastK / 4];     // regenerate: replica erased[w] (nullptr: not requested)
+  uint64_t out_len;                  // restore: E bytes to write
+  uint64_t chunk_len;                // L = 2 T + 2 bytes of every survivor (and regenerated replica)
+  uint32_t first_tile;               // the object's first tile in the batch
+  uint32_t plan;                     // its erased set's entry in plans[]
+  uint8_t point[kMaxFastK];          // survivor j's point
+};
+struct SynBatchPlan {
+  uint8_t erased[kMaxFastK / 4];
+  uint32_t solve_sel[kMaxFastK / 4][4];  // as SynRestoreArgs::solve_sel
+};
+
 hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s);
 bool has_restore_syn(uint32_t k, uint32_t n);
 // W[j][a] = v_a a^j of the syndrome map for (k, n); nullptr if not compiled.
 const uint16_t *restore_syn_weights(uint32_t k, uint32_t n);
 hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen = false);
+// a.objs / a.plans / a.tile_obj / a.total_tiles set; the other fields unused
+hipError_t launch_restore_syn_batch(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen);
 hipError_t launch_regen_generic(const RegenArgs &a, hipStream_t s);
 hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s);
 // Returns hipErrorNotSupported when no bit-sliced instantiation exists for (k, n).

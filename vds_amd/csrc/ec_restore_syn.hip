@@ -12,6 +12,8 @@
 //   4. big-endian stores through an LDS staging of the tile.
 // REGEN stops after step 2 and writes the recovered points as replica bytes:
 // the fused repair of sync_process.cpp:313-335 (decode + re-encode).
+#include <climits>
+
 #include "ec_device.hpp"
 
 namespace vds_ec {
@@ -214,6 +216,33 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
   }
 }
 
+// Batch mode: the last tile of an object may run past its bytes.  Loads
+// beyond `valid` bytes read zeros and stores beyond it write nothing (byte by
+// byte for the one 16-byte piece that straddles the end).
+__device__ __forceinline__ u32x4 ld16_guard(const uint8_t *p, int64_t valid) {
+  if (valid >= 16) return g_ld<4, u32x4>(p);
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (valid > 0) {  // (chunk lengths are even: whole dwords, then a 2-byte cell)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (4 * i + 4 <= valid) v[i] = *reinterpret_cast<const uint32_t *>(p + 4 * i);
+    if (valid & 2) v[valid >> 2] = *reinterpret_cast<const uint16_t *>(p + (valid & ~3));
+  }
+  return v;
+}
+__device__ __forceinline__ void st16_guard(uint8_t *p, u32x4 v, int64_t valid) {
+  if (valid >= 16) {
+    g_st<8>(p, v);
+  } else if (valid > 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (4 * i + 4 <= valid) *reinterpret_cast<uint32_t *>(p + 4 * i) = v[i];
+    const int w = (int)(valid >> 2);
+    const uint32_t x = v[w];
+    for (int b = 0; b < (int)(valid & 3); ++b) p[4 * w + b] = uint8_t(x >> (8 * b));
+  }
+}
+
 // Restore of an object from any K of its N replicas without a per-pattern
 // K x K inverse (tools/xorgen/gen_restore.cpp).  Per tile, wave w:
 //  1. loads survivors kLoadPer*w.. into their points' planes (waves < M also
@@ -224,7 +253,10 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
 //     them big-endian.
 // Tiles are strided over the grid (one contiguous range of tiles per
 // workgroup measured slower: repair 1572 -> 1460 GiB/s).
-template <int K, int N, int WV, bool REGEN>
+// BATCH: one launch over the tiles of many objects, each with its own
+// survivors, erasure plan, size and output (SynBatchObj / SynBatchPlan:
+// wave-uniform scalar loads per tile); the last tile of an object is guarded.
+template <int K, int N, int WV, bool REGEN, bool BATCH>
 __global__ __launch_bounds__((SynShape<K, N, WV>::kThreads), (SynShape<K, N, WV>::kWavesPerSimd))
 void k_restore_syn(SynRestoreArgs a) {
   using S = SynShape<K, N, WV>;
@@ -244,20 +276,33 @@ void k_restore_syn(SynRestoreArgs a) {
   } else {
     L.hi2 = L.hi;
   }
-  const int my_erased = wave < S::kM ? a.erased[wave] : 0;
+  // per-tile data: the launch's (uniform) or the tile's object's (batch)
+  auto obj_of = [&](uint32_t t) -> uint32_t { return BATCH ? a.tile_obj[t] : t / a.tiles_per_obj; };
+  auto stripe0_of = [&](uint32_t t, uint32_t o) -> uint64_t {
+    return (uint64_t)(BATCH ? t - a.objs[o].first_tile : t % a.tiles_per_obj) * kTileStripes;
+  };
+  auto erased_of = [&](uint32_t o, int m) -> int { return BATCH ? a.plans[a.objs[o].plan].erased[m] : a.erased[m]; };
 
   // survivor staging: the next tile's loads are issued after the syndrome
   // programs (k = 32: after the interpolation, see kLateLoad) and land while
   // the rest of this tile runs
   u32x4 Q[S::kLoadPer][4];
   auto load = [&](uint32_t t) {
-    const uint32_t ob = t / a.tiles_per_obj;
-    const uint64_t st0 = (uint64_t)(t % a.tiles_per_obj) * kTileStripes;
+    const uint32_t ob = obj_of(t);
+    const uint64_t st0 = stripe0_of(t, ob);
 #pragma unroll
     for (int s = 0; s < S::kLoadPer; ++s) {
-      const uint8_t *src = a.chunks[wave * S::kLoadPer + s] + (uint64_t)ob * a.chunk_stride + 2 * st0 + 16 * lane;
+      if constexpr (BATCH) {
+        const SynBatchObj &d = a.objs[ob];
+        const uint8_t *src = d.chunks[wave * S::kLoadPer + s] + 2 * st0 + 16 * lane;
+        const int64_t valid = (int64_t)(d.chunk_len - 2 * st0) - 16 * lane;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Q[s][q] = g_ld<4, u32x4>(src + 1024 * q);
+        for (int q = 0; q < 4; ++q) Q[s][q] = ld16_guard(src + 1024 * q, valid - 1024 * q);
+      } else {
+        const uint8_t *src = a.chunks[wave * S::kLoadPer + s] + (uint64_t)ob * a.chunk_stride + 2 * st0 + 16 * lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Q[s][q] = g_ld<4, u32x4>(src + 1024 * q);
+      }
     }
   };
   // The next tile's survivors, or zeros past the last tile: both paths define
@@ -280,7 +325,9 @@ void k_restore_syn(SynRestoreArgs a) {
   // live across the syndrome and stage-B programs, which then spill; they are
   // issued after the interpolation instead and land under the staging and
   // stores (REGEN has no interpolation and keeps the early issue)
-  constexpr bool kLateLoad = K == 32 && !REGEN;
+  // (batch: the guarded loads and descriptor addresses would not fit beside
+  // the programs either)
+  constexpr bool kLateLoad = (K == 32 || BATCH) && !REGEN;
   const uint32_t t_step = gridDim.x;
   prefetch(blockIdx.x);
   // vmcnt counts loads and stores together and retires them in issue order.
@@ -293,7 +340,7 @@ void k_restore_syn(SynRestoreArgs a) {
   // stores to complete.  Issuing the same 16 stores here (zeros into this
   // wave's copy-out chunk of its first tile, which that tile's copy-out
   // overwrites, in order, from the same wave) makes both states alike.
-  if constexpr (!REGEN) {
+  if constexpr (!REGEN && !BATCH) {  // (batch: guarded stores; nothing to mirror)
     if (blockIdx.x < a.total_tiles) {
       const uint32_t t0 = blockIdx.x;
       uint8_t *g0 = a.out + (uint64_t)(t0 / a.tiles_per_obj) * a.out_stride +
@@ -303,8 +350,9 @@ void k_restore_syn(SynRestoreArgs a) {
     }
   }
   for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += t_step) {
-    const uint32_t o = tile / a.tiles_per_obj;
-    const uint64_t stripe0 = (uint64_t)(tile % a.tiles_per_obj) * kTileStripes;
+    const uint32_t o = obj_of(tile);
+    const uint64_t stripe0 = stripe0_of(tile, o);
+    const int my_erased = wave < S::kM ? erased_of(o, wave) : 0;
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
     {
       if (wave < S::kM) {
@@ -323,7 +371,7 @@ void k_restore_syn(SynRestoreArgs a) {
         uint32_t Pl[16];
 #pragma unroll
         for (int b = 0; b < 16; ++b) Pl[b] = W[b ^ 8];
-        syn_put_point(L, a.point[wave * S::kLoadPer + s], Pl);
+        syn_put_point(L, BATCH ? a.objs[o].point[wave * S::kLoadPer + s] : a.point[wave * S::kLoadPer + s], Pl);
       }
     }
     st.mark(0);
@@ -359,7 +407,8 @@ void k_restore_syn(SynRestoreArgs a) {
           const Plane16 t1 = plane_mulx(tt);
 #pragma unroll
           for (int m = 0; m < kMC; ++m) {
-            const uint32_t two = (a.solve_sel[m0 + m][b >> 2] >> (8 * (b & 3) + wave)) & 0x101u;
+            const uint32_t sel = BATCH ? a.plans[a.objs[o].plan].solve_sel[m0 + m][b >> 2] : a.solve_sel[m0 + m][b >> 2];
+            const uint32_t two = (sel >> (8 * (b & 3) + wave)) & 0x101u;
             if (two == 1u)
               ce[m] = plane_xor(ce[m], tt);
             else if (two == 0x100u)
@@ -375,7 +424,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #pragma unroll
         for (int m = 0; m < kMC; ++m) {
           __attribute__((address_space(3))) uint64_t *dst =
-              (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * a.erased[m0 + m]);
+              (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * erased_of(o, m0 + m));
 #pragma unroll
           for (int h = 0; h < 8; ++h)
             __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1),
@@ -392,16 +441,27 @@ void k_restore_syn(SynRestoreArgs a) {
       // (P(e_w) stripe by stripe).  Undo the stage-1 transpose and store it as
       // big-endian cells, one 1 KiB store per wave-instruction; no
       // interpolation (fused "decode + re-encode" of sync_process.cpp:313-335).
-      if (wave < S::kM && a.regen[wave] != nullptr) {
+      uint8_t *const rg = wave < S::kM ? (BATCH ? a.objs[o].regen[wave] : a.regen[wave]) : nullptr;
+      if (rg != nullptr) {
         uint32_t Pl[16], W[16];
         syn_get_point(L, my_erased, Pl);
 #pragma unroll
         for (int b = 0; b < 16; ++b) W[b ^ 8] = Pl[b];
         transpose16x2(W, bm);  // self-inverse: back to the loaded word layout
-        uint8_t *dst = a.regen[wave] + (uint64_t)o * a.regen_stride + 2 * stripe0 + 16 * lane;
+        if constexpr (BATCH) {
+          // the whole replica, trailer included: every survivor holds the
+          // trailer value p at cell T, so the recovered cell T is p as well
+          uint8_t *dst = rg + 2 * stripe0 + 16 * lane;
+          const int64_t valid = (int64_t)(a.objs[o].chunk_len - 2 * stripe0) - 16 * lane;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          g_st<8>(dst + 1024 * q, u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]});
+          for (int q = 0; q < 4; ++q)
+            st16_guard(dst + 1024 * q, u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]}, valid - 1024 * q);
+        } else {
+          uint8_t *dst = rg + (uint64_t)o * a.regen_stride + 2 * stripe0 + 16 * lane;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            g_st<8>(dst + 1024 * q, u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]});
+        }
       }
       __syncthreads();  // every wave is done with this tile's planes
       continue;
@@ -410,8 +470,10 @@ void k_restore_syn(SynRestoreArgs a) {
     {
       uint32_t cells[16 * S::kCells];
       syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
-      if (kLateLoad) prefetch(tile + t_step);
-      uint8_t *dst = a.out + (uint64_t)o * a.out_stride;
+      if (kLateLoad && !BATCH) prefetch(tile + t_step);
+      uint8_t *dst = BATCH ? a.objs[o].out : a.out + (uint64_t)o * a.out_stride;
+      // batch: bytes of this tile's output still inside the object's E bytes
+      const int64_t out_valid = BATCH ? (int64_t)a.objs[o].out_len - (int64_t)(stripe0 * (2 * K)) : INT64_MAX;
       constexpr int kGroups = S::kCells / 2;  // word groups (2 cells) per wave
       if constexpr (K == 16) {
         // Stage the tile's output in LDS (the planes are dead once every wave
@@ -447,6 +509,7 @@ void k_restore_syn(SynRestoreArgs a) {
               u32x2{rows[0][pi], rows[1][pi]};
         }
         st.mark(15);
+        if (BATCH) prefetch(tile + t_step);  // (batch: the staged rows are dead; room for the survivors)
         __syncthreads();
         st.mark(16);
         // 16-byte chunk c = 64 (kChunks wave + i) + lane of the tile: stripe c/2,
@@ -459,7 +522,11 @@ void k_restore_syn(SynRestoreArgs a) {
           const lds_char *r = r0 + 1056 * i;
           const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
           const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
-          g_st<8>(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]});
+          if constexpr (BATCH)
+            st16_guard(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]},
+                       out_valid - (int64_t)(1024u * kChunks * wave + 16u * lane + 1024 * i));
+          else
+            g_st<8>(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]});
         }
         st.mark(17);
       } else {
@@ -491,6 +558,7 @@ void k_restore_syn(SynRestoreArgs a) {
           }
         }
         st.mark(15);
+        if (BATCH) prefetch(tile + t_step);  // (batch: the staged rows are dead; room for the survivors)
         __syncthreads();
         st.mark(16);
         // 16-byte chunk c = 64 (16 wave + i) + lane of the tile: stripe c/4,
@@ -503,7 +571,11 @@ void k_restore_syn(SynRestoreArgs a) {
           const lds_char *r = r0 + 1040 * i;
           const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
           const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
-          g_st<8>(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]});
+          if constexpr (BATCH)
+            st16_guard(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]},
+                       out_valid - (int64_t)(16384u * wave + 16u * lane + 1024 * i));
+          else
+            g_st<8>(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]});
         }
         st.mark(17);
       }
@@ -531,10 +603,10 @@ const uint16_t *restore_syn_weights(uint32_t k, uint32_t n) {
   return nullptr;
 }
 
-template <int K, int N, int WV, bool REGEN>
+template <int K, int N, int WV, bool REGEN, bool BATCH = false>
 static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) {
   using S = SynShape<K, N, WV>;
-  hipError_t e = ensure_lds_attr(&k_restore_syn<K, N, WV, REGEN>, S::kLdsBytes);
+  hipError_t e = ensure_lds_attr(&k_restore_syn<K, N, WV, REGEN, BATCH>, S::kLdsBytes);
   if (e != hipSuccess) return e;
   const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
   uint32_t grid = 256u * (blocks_per_cu > 0 ? blocks_per_cu : 1);
@@ -542,7 +614,7 @@ static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) 
   if (over) grid = over;
   if (grid > a.total_tiles) grid = a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_restore_syn<K, N, WV, REGEN>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  hipLaunchKernelGGL((k_restore_syn<K, N, WV, REGEN, BATCH>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
   return hipGetLastError();
 }
 
@@ -551,6 +623,14 @@ hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, h
     return regen ? launch_restore_syn_kn<16, 20, 4, true>(a, s) : launch_restore_syn_kn<16, 20, 4, false>(a, s);
   if (k == 32 && n == 40)
     return regen ? launch_restore_syn_kn<32, 40, 8, true>(a, s) : launch_restore_syn_kn<32, 40, 8, false>(a, s);
+  return hipErrorNotSupported;
+}
+
+hipError_t launch_restore_syn_batch(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen) {
+  if (k == 16 && n == 20)
+    return regen ? launch_restore_syn_kn<16, 20, 4, true, true>(a, s) : launch_restore_syn_kn<16, 20, 4, false, true>(a, s);
+  if (k == 32 && n == 40)
+    return regen ? launch_restore_syn_kn<32, 40, 8, true, true>(a, s) : launch_restore_syn_kn<32, 40, 8, false, true>(a, s);
   return hipErrorNotSupported;
 }
 

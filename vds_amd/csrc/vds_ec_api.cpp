@@ -828,6 +828,184 @@ int check_restore_args(uint32_t k, const Id *nodes, const uint8_t *const *chunks
   return VDS_EC_OK;
 }
 
+// ------------------------------------------------ batched device restore
+// Many objects, each with its own survivor set, size and output, as the
+// download and repair loops meet them (restore_async gathers the first k
+// replicas found PER OBJECT, dht_network_client.cpp:851-901; sync_process
+// repairs object by object, sync_process.cpp:313-335).  Objects whose
+// survivors lie within the syndrome kernel's points go to ONE launch of
+// k_restore_syn in batch mode, over every tile of every such object; the
+// erasure plan (M x M solve) is computed once per distinct erased set.  Other
+// objects fall back to one restore_device / regenerate_device call each, on
+// the same stream.  Nothing synchronises.
+struct BatchPlanCache {
+  std::vector<SynBatchPlan> plans;
+  std::vector<std::pair<uint64_t, uint32_t>> keys;  // erased-set bitmask -> plan index
+  int find_or_add(uint64_t key, const SynRestoreArgs &sa, uint32_t m) {
+    for (auto &kv : keys)
+      if (kv.first == key) return (int)kv.second;
+    SynBatchPlan p{};
+    for (uint32_t i = 0; i < m; ++i) p.erased[i] = sa.erased[i];
+    std::memcpy(p.solve_sel, sa.solve_sel, sizeof p.solve_sel);
+    plans.push_back(p);
+    keys.push_back({key, (uint32_t)plans.size() - 1});
+    return (int)plans.size() - 1;
+  }
+};
+
+// Stage the batch tables (objects, plans, tile -> object) and launch.
+int launch_syn_batch(uint32_t k, uint32_t n, const std::vector<SynBatchObj> &objs, const BatchPlanCache &pc,
+                     const std::vector<uint32_t> &tile_obj, bool regen, hipStream_t s) {
+  if (tile_obj.empty()) return VDS_EC_OK;
+  std::vector<uint8_t> blob;
+  const size_t o_objs = blob_append(blob, objs.data(), objs.size());
+  const size_t o_plans = blob_append(blob, pc.plans.data(), pc.plans.size());
+  const size_t o_tiles = blob_append(blob, tile_obj.data(), tile_obj.size());
+  const uint8_t *d = nullptr;
+  ParamSlot *slot = nullptr;
+  hipError_t e = param_stage(blob, s, &d, &slot);
+  if (e == hipSuccess) {
+    SynRestoreArgs sa{};
+    sa.objs = reinterpret_cast<const SynBatchObj *>(d + o_objs);
+    sa.plans = reinterpret_cast<const SynBatchPlan *>(d + o_plans);
+    sa.tile_obj = reinterpret_cast<const uint32_t *>(d + o_tiles);
+    sa.total_tiles = (uint32_t)tile_obj.size();
+    e = launch_restore_syn_batch(k, n, sa, s, regen);
+  }
+  if (slot) {
+    const hipError_t re = param_release(slot, s);
+    if (e == hipSuccess) e = re;
+  }
+  return hip_status(e);
+}
+
+int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
+                         const uint64_t *chunk_sizes, const uint16_t *paddings, uint8_t *const *outs, unsigned flags,
+                         hipStream_t s) {
+  if (k == 0 || (count && (!nodes || !chunks || !chunk_sizes || !paddings || !outs))) return VDS_EC_EINVAL;
+  if (count == 0) return VDS_EC_OK;
+  // every object is validated before anything is enqueued
+  std::vector<uint64_t> lens(count);
+  for (uint32_t o = 0; o < count; ++o) {
+    int rc = check_restore_args(k, nodes + (uint64_t)o * k, chunks + (uint64_t)o * k, chunk_sizes[o]);
+    if (rc) return rc;
+    bool ok = true;
+    lens[o] = restored_len(2, k, chunk_sizes[o], paddings[o], flags, &ok);
+    if (!ok) return VDS_EC_ERESTORE;
+    if (lens[o] && !outs[o]) return VDS_EC_EINVAL;
+  }
+  int rc = device_ready();
+  if (rc) return rc;
+  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
+  const uint32_t n = k + k / 4;
+  std::vector<SynBatchObj> objs;
+  std::vector<uint32_t> tile_obj;
+  BatchPlanCache pc;
+  std::vector<uint32_t> fallback;
+  for (uint32_t o = 0; o < count; ++o) {
+    const uint16_t *nd = nodes + (uint64_t)o * k;
+    SynRestoreArgs sa{};
+    uint32_t syn_n = 0;
+    const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);  // stripes that produce output
+    if (cells || !plan_restore_syn(k, nd, sa, &syn_n) || syn_n != n) {
+      fallback.push_back(o);
+      continue;
+    }
+    if (need == 0) continue;
+    uint64_t key = 0;
+    for (uint32_t i = 0; i < n - k; ++i) key |= 1ull << sa.erased[i];
+    SynBatchObj d{};
+    for (uint32_t j = 0; j < k; ++j) {
+      d.chunks[j] = chunks[(uint64_t)o * k + j];
+      d.point[j] = sa.point[j];
+    }
+    d.out = outs[o];
+    d.out_len = lens[o];
+    d.chunk_len = chunk_sizes[o];
+    d.plan = (uint32_t)pc.find_or_add(key, sa, n - k);
+    d.first_tile = (uint32_t)tile_obj.size();
+    const uint64_t tiles = (need + kTileStripes - 1) / kTileStripes;
+    if (tile_obj.size() + tiles > 0xFFFFFFFFull) return VDS_EC_EINVAL;
+    tile_obj.insert(tile_obj.end(), tiles, (uint32_t)objs.size());
+    objs.push_back(d);
+  }
+  rc = launch_syn_batch(k, n, objs, pc, tile_obj, false, s);
+  if (rc) return rc;
+  for (uint32_t o : fallback) {
+    if (lens[o] == 0) continue;
+    std::vector<uint16_t> m((size_t)k * k);
+    rc = inverse16(k, nodes + (uint64_t)o * k, m.data());
+    if (rc) return rc;
+    rc = restore_device(2, k, nodes + (uint64_t)o * k, m.data(), chunks + (uint64_t)o * k, chunk_sizes[o], 0, lens[o], 1,
+                        outs[o], 0, flags, s);
+    if (rc) return rc;
+  }
+  return VDS_EC_OK;
+}
+
+int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
+                            const uint64_t *chunk_sizes, uint32_t nt, const uint16_t *targets, uint8_t *const *outs,
+                            hipStream_t s) {
+  if (k == 0 || (count && (!nodes || !chunks || !chunk_sizes || (nt && (!targets || !outs))))) return VDS_EC_EINVAL;
+  if (count == 0 || nt == 0) return VDS_EC_OK;
+  for (uint32_t o = 0; o < count; ++o) {
+    if (chunk_sizes[o] < 2 || (chunk_sizes[o] - 2) % 2) return VDS_EC_EINVAL;  // cells + BE16 trailer
+    for (uint32_t j = 0; j < k; ++j)
+      if (!chunks[(uint64_t)o * k + j]) return VDS_EC_EINVAL;
+    for (uint32_t i = 0; i < nt; ++i)
+      if (!outs[(uint64_t)o * nt + i]) return VDS_EC_EINVAL;
+  }
+  int rc = device_ready();
+  if (rc) return rc;
+  const uint32_t n = k + k / 4;
+  std::vector<SynBatchObj> objs;
+  std::vector<uint32_t> tile_obj;
+  BatchPlanCache pc;
+  std::vector<uint32_t> fallback;
+  for (uint32_t o = 0; o < count; ++o) {
+    const uint16_t *nd = nodes + (uint64_t)o * k;
+    SynRestoreArgs sa{};
+    uint32_t syn_n = 0;
+    bool syn = plan_restore_syn(k, nd, sa, &syn_n) && syn_n == n;
+    SynBatchObj d{};
+    for (uint32_t i = 0; syn && i < nt; ++i) {  // every target must be one of the erased points
+      bool hit = false;
+      for (uint32_t w = 0; w < n - k && !hit; ++w)
+        if (sa.erased[w] == targets[(uint64_t)o * nt + i] && !d.regen[w]) {
+          d.regen[w] = outs[(uint64_t)o * nt + i];
+          hit = true;
+        }
+      syn = hit;
+    }
+    if (!syn) {
+      fallback.push_back(o);
+      continue;
+    }
+    uint64_t key = 0;
+    for (uint32_t i = 0; i < n - k; ++i) key |= 1ull << sa.erased[i];
+    for (uint32_t j = 0; j < k; ++j) {
+      d.chunks[j] = chunks[(uint64_t)o * k + j];
+      d.point[j] = sa.point[j];
+    }
+    d.chunk_len = chunk_sizes[o];
+    d.plan = (uint32_t)pc.find_or_add(key, sa, n - k);
+    d.first_tile = (uint32_t)tile_obj.size();
+    const uint64_t cells_t = chunk_sizes[o] / 2;  // T cells + the trailer cell
+    const uint64_t tiles = (cells_t + kTileStripes - 1) / kTileStripes;
+    if (tile_obj.size() + tiles > 0xFFFFFFFFull) return VDS_EC_EINVAL;
+    tile_obj.insert(tile_obj.end(), tiles, (uint32_t)objs.size());
+    objs.push_back(d);
+  }
+  rc = launch_syn_batch(k, n, objs, pc, tile_obj, true, s);
+  if (rc) return rc;
+  for (uint32_t o : fallback) {
+    rc = regenerate_device(2, k, nodes + (uint64_t)o * k, chunks + (uint64_t)o * k, chunk_sizes[o], 0, 1,
+                           targets + (uint64_t)o * nt, nt, outs + (uint64_t)o * nt, 0, s);
+    if (rc) return rc;
+  }
+  return VDS_EC_OK;
+}
+
 // ------------------------------------------------- multi-GPU host batch
 // Pinned staging of the host batch path, one ring per device, created on
 // first use and kept (like HostCtx): hipHostMalloc of hundreds of MiB costs
@@ -1378,6 +1556,18 @@ int vds_ec_regenerate16_device(uint16_t k, const uint16_t *nodes, const uint8_t 
 int vds_ec_regenerate16_host(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
                              const uint16_t *targets, uint32_t ntargets, uint8_t *const *outs) {
   return regenerate_host(2, k, nodes, chunks, chunk_size, targets, ntargets, outs);
+}
+
+int vds_ec_restore16_batch_device(uint16_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
+                                  const uint64_t *chunk_sizes, const uint16_t *paddings, uint8_t *const *outs,
+                                  unsigned flags, void *stream) {
+  return restore_batch_device(k, count, nodes, chunks, chunk_sizes, paddings, outs, flags, as_stream(stream));
+}
+
+int vds_ec_regenerate16_batch_device(uint16_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
+                                     const uint64_t *chunk_sizes, uint32_t ntargets, const uint16_t *targets,
+                                     uint8_t *const *outs, void *stream) {
+  return regenerate_batch_device(k, count, nodes, chunks, chunk_sizes, ntargets, targets, outs, as_stream(stream));
 }
 
 int vds_ec_regenerate16_path(uint16_t k, const uint16_t *nodes, const uint16_t *targets, uint32_t ntargets,

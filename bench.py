@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--object-mib", type=float, default=64.0)
     p.add_argument("--erase", type=str, default="", help="comma list of erased replica ids")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-live", action="store_true", help="skip the live-shape line (k=32, n=64, 64 KiB objects)")
+    p.add_argument("--live-objects", type=int, default=16384)
     p.add_argument("--cpu-objects", type=int, default=8, help="objects in the CPU baseline sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-object HBM bytes per kernel from rocprofv3 PMC passes (tools/pmc_traffic.py)")
@@ -156,6 +158,100 @@ def max_over_ranks(values, dist, device):
     t = torch.tensor(list(values), dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t.tolist()]
+
+
+def live_shape(torch, chunk, dev, stream, objects, steps, loss=0.02, seed=1):
+    """The production shape beside the metric (never in it): MIN_HORCRUX 32,
+    GENERATE_HORCRUX 64 (dht_network.h:22-25) on the web client's 64 KiB
+    blocks (web/src/store/vds_api.jsx:76).  Encode all 64 replicas of every
+    object (save_temp); then every replica is lost independently with
+    probability `loss`, each object is restored from the first 32 replicas
+    found (restore_async, dht_network_client.cpp:851-901) with ONE batched
+    call over all objects (vds_ec_restore16_batch_device), and one lost
+    replica of 0..39 per object is regenerated (sync_process's repair) with
+    vds_ec_regenerate16_batch_device.  Host times include the per-object
+    planning and table staging of the batched calls."""
+    import ctypes as C
+    import numpy as np
+    from vds_amd import _lib
+    k, n, size = 32, 64, 65536
+    L = chunk.replica_size(k, size)
+    inp = torch.empty(objects * size, dtype=torch.uint8, device=dev)
+    chunk.fill_splitmix_device(inp, objects * size, SEED ^ 0x6C697665)
+    reps = torch.empty((n, objects * L), dtype=torch.uint8, device=dev)
+    out = torch.empty(objects * size, dtype=torch.uint8, device=dev)
+    rep_ptrs = [reps[i].data_ptr() for i in range(n)]
+
+    def enc():
+        chunk.encode_device(k, list(range(n)), inp, size, size, objects, rep_ptrs, L)
+
+    rng = np.random.default_rng(seed)
+    lost = rng.random((objects, n)) < loss
+    ok = (~lost).sum(axis=1) >= k
+    objs = np.flatnonzero(ok)
+    nodes = np.stack([np.flatnonzero(~lost[o])[:k] for o in objs]).astype(np.uint16)
+    base = np.asarray(rep_ptrs, dtype=np.uint64)
+    chunk_ptrs = (base[nodes] + (objs.astype(np.uint64) * L)[:, None]).astype(np.uint64)
+    sizes = np.full(len(objs), L, dtype=np.uint64)
+    pads = np.zeros(len(objs), dtype=np.uint16)
+    outs = (np.uint64(out.data_ptr()) + objs.astype(np.uint64) * size).astype(np.uint64)
+    lib = _lib.lib()
+    sp = stream.cuda_stream
+
+    def restore():
+        _lib.check(lib.vds_ec_restore16_batch_device(
+            k, len(objs), nodes.ctypes.data_as(_lib.u16p), chunk_ptrs.ctypes.data_as(_lib.vpp),
+            sizes.ctypes.data_as(_lib.u64p), pads.ctypes.data_as(_lib.u16p), outs.ctypes.data_as(_lib.vpp), 0, sp))
+
+    # regenerate: objects that lost a replica among 0..39, its first such id
+    low_lost = lost[objs, :40]
+    rg = np.flatnonzero(low_lost.any(axis=1))
+    rg_targets = np.argmax(low_lost[rg], axis=1).astype(np.uint16)
+    rg_out = torch.empty(max(1, len(rg)) * L, dtype=torch.uint8, device=dev)
+    rg_outs = (np.uint64(rg_out.data_ptr()) + np.arange(len(rg), dtype=np.uint64) * L).astype(np.uint64)
+    rg_nodes = np.ascontiguousarray(nodes[rg])
+    rg_chunks = np.ascontiguousarray(chunk_ptrs[rg])
+    rg_sizes = np.full(len(rg), L, dtype=np.uint64)
+
+    def regen():
+        _lib.check(lib.vds_ec_regenerate16_batch_device(
+            k, len(rg), rg_nodes.ctypes.data_as(_lib.u16p), rg_chunks.ctypes.data_as(_lib.vpp),
+            rg_sizes.ctypes.data_as(_lib.u64p), 1, rg_targets.ctypes.data_as(_lib.u16p),
+            rg_outs.ctypes.data_as(_lib.vpp), sp))
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(steps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / steps, e0.elapsed_time(e1) / steps * 1e-3
+
+    with torch.cuda.stream(stream):
+        enc_wall, enc_gpu = timed(enc)
+        rest_wall, rest_gpu = timed(restore)
+        regen_wall, regen_gpu = timed(regen) if len(rg) else (None, None)
+    torch.cuda.synchronize(dev)
+    idx = torch.from_numpy(objs).to(dev)
+    assert torch.equal(out.view(objects, size)[idx], inp.view(objects, size)[idx]), "live restore differs"
+    if len(rg):  # the regenerated replicas equal the encoded ones
+        want = torch.stack([reps[int(t), int(o) * L:(int(o) + 1) * L] for t, o in zip(rg_targets[:64], objs[rg[:64]])])
+        assert torch.equal(rg_out.view(-1, L)[:64], want), "live regenerate differs"
+    gib = lambda nbytes, t: round(nbytes / t / 2**30, 3) if t else None
+    res = {"shape": f"k={k}, n={n}, {objects} x 64 KiB objects; replica loss p={loss}; "
+                    f"{len(objs)} restorable, {len(rg)} regenerated",
+           "encode_GiBps": gib(objects * size, enc_gpu),
+           "repair_GiBps": gib(len(objs) * size, rest_gpu),
+           "repair_host_GiBps": gib(len(objs) * size, rest_wall),
+           "regenerate_GiBps": gib(len(rg) * size, regen_gpu),
+           "regenerate_host_GiBps": gib(len(rg) * size, regen_wall),
+           "distinct_survivor_sets": int(len({tuple(r) for r in nodes.tolist()}))}
+    del inp, reps, out, rg_out
+    return res
 
 
 def main():
@@ -296,6 +392,12 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.traffic_json, dom, objects, k, n)
 
+    live = None
+    if not args.no_live:
+        del inp, restored, reps, digests, regen_out
+        torch.cuda.empty_cache()
+        live = live_shape(torch, chunk, dev, torch.cuda.Stream(dev), args.live_objects, args.steps)
+
     result = {
         "metric": "device-resident encode+repair GiB/s, k=16 m=4 64 MiB stripes, 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -324,6 +426,7 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "traffic_source": traffic_src, "algorithmic_bytes_per_launch": dom_bytes,
                      "avg_launch_ms": round(dom_ms, 4), "kernels": {"encode": enc_name, "repair": rep_name}},
+        "live_shape": live,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -40,8 +40,8 @@ def test_restore_batch_per_object_survivors(gpu, k, n_total):
     from vds_amd import chunk
     rng = np.random.default_rng(k * 100 + n_total)
     tile = 2048 * 2 * k
-    sizes = [0, 1, 2 * k, 2 * k * 7 + 3, tile - 1, tile, tile + 5, 2 * tile + 2 * k * 3 + 1, 65536, 58113,
-             3 * tile + 11] + [int(x) for x in rng.integers(1, 3 * tile, 9)]
+    sizes = [0, 1, 2 * k, 2 * k * 7 + 3, tile // 2 - 1, tile // 2, tile // 2 + 1, tile - 1, tile, tile + 5,
+             2 * tile + 2 * k * 3 + 1, 65536, 58113, 3 * tile + 11] + [int(x) for x in rng.integers(1, 3 * tile, 9)]
     objs = _objects(torch, k, n_total, sizes, seed=k)
     nodes, chunks, csz, pads, outs = [], [], [], [], []
     for (host, reps), size in zip(objs, sizes):
@@ -70,7 +70,7 @@ def test_regenerate_batch_per_object(gpu, k, n_total):
     from vds_amd import chunk
     rng = np.random.default_rng(7 + k + n_total)
     tile = 2048 * 2 * k
-    sizes = [1, 2 * k * 9 + 1, tile, tile + 2 * k, 2 * tile + 7, 65536] + [int(x) for x in rng.integers(1, 2 * tile, 6)]
+    sizes = [1, 2 * k * 9 + 1, tile // 2 - 2 * k, tile // 2, tile // 2 + 1, tile, tile + 2 * k, 2 * tile + 7, 65536] + [int(x) for x in rng.integers(1, 2 * tile, 6)]
     objs = _objects(torch, k, n_total, sizes, seed=500 + k)
     nt = 2
     nodes, chunks, csz, targets, outs = [], [], [], [], []
@@ -106,3 +106,33 @@ def test_restore_batch_rejects_bad_objects(gpu):
         chunk.restore_batch_device(k, [nd, nd], [[reps[r].data_ptr() for r in nd]] * 2, [reps[0].numel()] * 2,
                                    [1000 % 32, 65535], [out.data_ptr()] * 2)
     assert e.value.status == ERESTORE
+
+
+@pytest.mark.parametrize("k,n_total", [(16, 20), (32, 64)])
+def test_batch_pairs_halves_of_small_objects(gpu, k, n_total):
+    """Many objects of half a tile or less sharing a few survivor sets: their
+    halves are paired into tiles across objects (odd counts leave an empty
+    half); restore and regenerate both checked object by object."""
+    import torch
+    from vds_amd import chunk
+    rng = np.random.default_rng(31 + k)
+    half = 1024 * 2 * k
+    sizes = [half] * 9 + [half - 2 * k * 5 - 3] * 4 + [int(x) for x in rng.integers(1, 3 * half, 12)]
+    objs = _objects(torch, k, n_total, sizes, seed=700 + k)
+    sets = [_first_k_found(rng, k, n_total, int(rng.integers(1, n_total - k + 1))) for _ in range(3)]
+    nodes = [sets[i % 3] if i % 5 else list(rng.permutation(sets[i % 3])) for i in range(len(sizes))]
+    chunks = [[reps[r].data_ptr() for r in nd] for (_, reps), nd in zip(objs, nodes)]
+    csz = [reps[0].numel() for _, reps in objs]
+    outs = [torch.full((size + 2 * k,), 0xA5, dtype=torch.uint8, device="cuda") for size in sizes]
+    chunk.restore_batch_device(k, nodes, chunks, csz, [sz % (2 * k) for sz in sizes], [o.data_ptr() for o in outs])
+    targets = [[min(r for r in range(n_total) if r not in nd)] for nd in nodes]
+    rg = [torch.full((c + 8,), 0x5A, dtype=torch.uint8, device="cuda") for c in csz]
+    chunk.regenerate_batch_device(k, nodes, chunks, csz, targets, [[o.data_ptr()] for o in rg])
+    torch.cuda.synchronize()
+    for (host, reps), size, out, tg, r, c in zip(objs, sizes, outs, targets, rg, csz):
+        got = out.cpu().numpy()
+        assert np.array_equal(got[:size], host), size
+        assert (got[size:] == 0xA5).all(), size
+        g = r.cpu().numpy()
+        assert np.array_equal(g[:c], O.encode(k, tg[0], host)), (size, tg)
+        assert (g[c:] == 0x5A).all()

@@ -29,15 +29,29 @@ typedef __attribute__((address_space(3))) char lds_char;
 // (512 x 64 MiB, 3 rounds): none 840, {1,4,8} 859, all four 856 GiB/s.
 constexpr int kNonTemporal = 1 | 4 | 8;
 
+// The pointers are global memory: the explicit address space keeps pointers
+// the kernel read from memory (batch descriptors) from becoming flat_
+// accesses, which also count against lgkmcnt and retire out of order.
+template <class T>
+using gmem = __attribute__((address_space(1))) T;
 template <int BIT, class T>
 __device__ __forceinline__ T g_ld(const void *p) {
-  if constexpr ((kNonTemporal & BIT) != 0) return __builtin_nontemporal_load(reinterpret_cast<const T *>(p));
-  else return *reinterpret_cast<const T *>(p);
+  const gmem<T> *q = (const gmem<T> *)p;
+  if constexpr ((kNonTemporal & BIT) != 0) return __builtin_nontemporal_load(q);
+  else return *q;
 }
 template <int BIT, class T>
 __device__ __forceinline__ void g_st(void *p, T v) {
-  if constexpr ((kNonTemporal & BIT) != 0) __builtin_nontemporal_store(v, reinterpret_cast<T *>(p));
-  else *reinterpret_cast<T *>(p) = v;
+  gmem<T> *q = (gmem<T> *)p;
+  if constexpr ((kNonTemporal & BIT) != 0) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
+// A wave-uniform read of a launch table the kernel never writes (batch
+// descriptors): the constant address space lets a uniform address become an
+// s_load into SGPRs instead of a per-lane vector load.
+template <class T>
+__device__ __forceinline__ T s_ld(const T *p) {
+  return *(const __attribute__((address_space(4))) T *)p;
 }
 
 // The 16 planes of one cell from LDS as four ds_read_b128.  A volatile

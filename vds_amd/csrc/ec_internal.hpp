@@ -112,7 +112,7 @@ struct SynRestoreArgs {
   // batch mode (launch_restore_syn_batch): everything per object from tables
   const struct SynBatchObj *objs;
   const struct SynBatchPlan *plans;
-  const uint32_t *tile_obj;
+  const struct SynBatchTile *tiles;
 };
 
 constexpr int kInlineCoef = 512;  // regenerate coefficients carried in the kernel arguments
@@ -141,21 +141,30 @@ struct RegenArgs {
 
 // Batched k_restore_syn (per-object survivor sets, sizes and outputs; one
 // launch over every tile of every object).  Device tables, built on the host:
-// objs[o] for each object, plans[p] for each distinct erased set, tile_obj[t]
-// = the object of tile t (an object's tiles are consecutive).
+// objs[o] per object (its survivors in its plan's point order), plans[p] per
+// distinct erased set, tiles[t] per tile.  A tile is two halves of
+// kHalfStripes stripes; each half is a stripe range of any object of the
+// tile's plan, so small objects (the live 64 KiB ones: 1024 stripes at
+// k = 32) pair up instead of filling half a tile each.
+constexpr uint32_t kHalfStripes = kTileStripes / 2;
 struct SynBatchObj {
-  const uint8_t *chunks[kMaxFastK];  // survivor j of the object (K used)
+  const uint8_t *chunks[kMaxFastK];  // survivor j = the chunk of plan point j (K used)
   uint8_t *out;                      // restore: the object's bytes
   uint8_t *regen[kMaxFastK / 4];     // regenerate: replica erased[w] (nullptr: not requested)
   uint64_t out_len;                  // restore: E bytes to write
   uint64_t chunk_len;                // L = 2 T + 2 bytes of every survivor (and regenerated replica)
-  uint32_t first_tile;               // the object's first tile in the batch
-  uint32_t plan;                     // its erased set's entry in plans[]
-  uint8_t point[kMaxFastK];          // survivor j's point
 };
 struct SynBatchPlan {
   uint8_t erased[kMaxFastK / 4];
+  uint8_t point[kMaxFastK];               // the survivors' points, ascending
   uint32_t solve_sel[kMaxFastK / 4][4];  // as SynRestoreArgs::solve_sel
+};
+struct SynBatchTile {
+  uint32_t obj[2];      // object of each half (an unused half: the batch's empty object)
+  uint32_t stripe0[2];  // its first stripe
+  uint32_t plan;
+  uint32_t trailer;     // regenerate: bit h = half h also copies its object's trailer cell
+  uint32_t pad_[2];
 };
 
 hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s);
@@ -163,7 +172,7 @@ bool has_restore_syn(uint32_t k, uint32_t n);
 // W[j][a] = v_a a^j of the syndrome map for (k, n); nullptr if not compiled.
 const uint16_t *restore_syn_weights(uint32_t k, uint32_t n);
 hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen = false);
-// a.objs / a.plans / a.tile_obj / a.total_tiles set; the other fields unused
+// a.objs / a.plans / a.tiles / a.total_tiles set; the other fields unused
 hipError_t launch_restore_syn_batch(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen);
 hipError_t launch_regen_generic(const RegenArgs &a, hipStream_t s);
 hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s);

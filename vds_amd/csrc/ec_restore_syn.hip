@@ -225,8 +225,8 @@ __device__ __forceinline__ u32x4 ld16_guard(const uint8_t *p, int64_t valid) {
   if (valid > 0) {  // (chunk lengths are even: whole dwords, then a 2-byte cell)
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-      if (4 * i + 4 <= valid) v[i] = *reinterpret_cast<const uint32_t *>(p + 4 * i);
-    if (valid & 2) v[valid >> 2] = *reinterpret_cast<const uint16_t *>(p + (valid & ~3));
+      if (4 * i + 4 <= valid) v[i] = *(const gmem<uint32_t> *)(p + 4 * i);
+    if (valid & 2) v[valid >> 2] = *(const gmem<uint16_t> *)(p + (valid & ~3));
   }
   return v;
 }
@@ -236,10 +236,10 @@ __device__ __forceinline__ void st16_guard(uint8_t *p, u32x4 v, int64_t valid) {
   } else if (valid > 0) {
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-      if (4 * i + 4 <= valid) *reinterpret_cast<uint32_t *>(p + 4 * i) = v[i];
+      if (4 * i + 4 <= valid) *(gmem<uint32_t> *)(p + 4 * i) = v[i];
     const int w = (int)(valid >> 2);
     const uint32_t x = v[w];
-    for (int b = 0; b < (int)(valid & 3); ++b) p[4 * w + b] = uint8_t(x >> (8 * b));
+    for (int b = 0; b < (int)(valid & 3); ++b) ((gmem<uint8_t> *)p)[4 * w + b] = uint8_t(x >> (8 * b));
   }
 }
 
@@ -254,8 +254,11 @@ __device__ __forceinline__ void st16_guard(uint8_t *p, u32x4 v, int64_t valid) {
 // Tiles are strided over the grid (one contiguous range of tiles per
 // workgroup measured slower: repair 1572 -> 1460 GiB/s).
 // BATCH: one launch over the tiles of many objects, each with its own
-// survivors, erasure plan, size and output (SynBatchObj / SynBatchPlan:
-// wave-uniform scalar loads per tile); the last tile of an object is guarded.
+// survivors, erasure plan, size and output (SynBatchTile / SynBatchObj /
+// SynBatchPlan, read with wave-uniform scalar loads).  Each half of a tile
+// (q = 0, 1 and q = 2, 3 of the loads; waves 0..WV/2-1 and WV/2.. of the
+// copy-out) is a stripe range of its own object; a half that runs past its
+// object's bytes takes the guarded loads and stores.
 template <int K, int N, int WV, bool REGEN, bool BATCH>
 __global__ __launch_bounds__((SynShape<K, N, WV>::kThreads), (SynShape<K, N, WV>::kWavesPerSimd))
 void k_restore_syn(SynRestoreArgs a) {
@@ -276,29 +279,45 @@ void k_restore_syn(SynRestoreArgs a) {
   } else {
     L.hi2 = L.hi;
   }
-  // per-tile data: the launch's (uniform) or the tile's object's (batch)
-  auto obj_of = [&](uint32_t t) -> uint32_t { return BATCH ? a.tile_obj[t] : t / a.tiles_per_obj; };
-  auto stripe0_of = [&](uint32_t t, uint32_t o) -> uint64_t {
-    return (uint64_t)(BATCH ? t - a.objs[o].first_tile : t % a.tiles_per_obj) * kTileStripes;
-  };
-  auto erased_of = [&](uint32_t o, int m) -> int { return BATCH ? a.plans[a.objs[o].plan].erased[m] : a.erased[m]; };
+  // per-tile data: the launch's (uniform), or in batch mode the tile
+  // record's (t and wave are uniform, so the s_ld reads are scalar loads)
+  auto obj_of = [&](uint32_t t) -> uint32_t { return t / a.tiles_per_obj; };
+  auto stripe0_of = [&](uint32_t t) -> uint64_t { return (uint64_t)(t % a.tiles_per_obj) * kTileStripes; };
+  auto half_obj = [&](uint32_t t, int h) -> const SynBatchObj & { return a.objs[s_ld(&a.tiles[t].obj[h])]; };
+  auto half_s0 = [&](uint32_t t, int h) -> uint64_t { return s_ld(&a.tiles[t].stripe0[h]); };
 
   // survivor staging: the next tile's loads are issued after the syndrome
   // programs (k = 32: after the interpolation, see kLateLoad) and land while
   // the rest of this tile runs
   u32x4 Q[S::kLoadPer][4];
   auto load = [&](uint32_t t) {
-    const uint32_t ob = obj_of(t);
-    const uint64_t st0 = stripe0_of(t, ob);
+    if constexpr (BATCH) {
 #pragma unroll
-    for (int s = 0; s < S::kLoadPer; ++s) {
-      if constexpr (BATCH) {
-        const SynBatchObj &d = a.objs[ob];
-        const uint8_t *src = d.chunks[wave * S::kLoadPer + s] + 2 * st0 + 16 * lane;
-        const int64_t valid = (int64_t)(d.chunk_len - 2 * st0) - 16 * lane;
+      for (int h = 0; h < 2; ++h) {
+        const SynBatchObj &d = half_obj(t, h);
+        const uint64_t st0 = half_s0(t, h);
+        // bytes of each survivor from this half's first cell on
+        const int64_t valid = (int64_t)s_ld(&d.chunk_len) - (int64_t)(2 * st0);
+        const uint8_t *src[S::kLoadPer];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) Q[s][q] = ld16_guard(src + 1024 * q, valid - 1024 * q);
-      } else {
+        for (int s = 0; s < S::kLoadPer; ++s) src[s] = s_ld(&d.chunks[wave * S::kLoadPer + s]) + 2 * st0 + 16 * lane;
+        if (valid >= 2 * (int64_t)kHalfStripes) {
+#pragma unroll
+          for (int s = 0; s < S::kLoadPer; ++s)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) Q[s][2 * h + q] = g_ld<4, u32x4>(src[s] + 1024 * q);
+        } else {
+#pragma unroll
+          for (int s = 0; s < S::kLoadPer; ++s)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) Q[s][2 * h + q] = ld16_guard(src[s] + 1024 * q, valid - 16 * lane - 1024 * q);
+        }
+      }
+    } else {
+      const uint32_t ob = obj_of(t);
+      const uint64_t st0 = stripe0_of(t);
+#pragma unroll
+      for (int s = 0; s < S::kLoadPer; ++s) {
         const uint8_t *src = a.chunks[wave * S::kLoadPer + s] + (uint64_t)ob * a.chunk_stride + 2 * st0 + 16 * lane;
 #pragma unroll
         for (int q = 0; q < 4; ++q) Q[s][q] = g_ld<4, u32x4>(src + 1024 * q);
@@ -350,9 +369,11 @@ void k_restore_syn(SynRestoreArgs a) {
     }
   }
   for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += t_step) {
-    const uint32_t o = obj_of(tile);
-    const uint64_t stripe0 = stripe0_of(tile, o);
-    const int my_erased = wave < S::kM ? erased_of(o, wave) : 0;
+    const uint32_t o = BATCH ? 0u : obj_of(tile);  // (non-batch)
+    const uint64_t stripe0 = BATCH ? 0u : stripe0_of(tile);
+    const SynBatchPlan *pl = BATCH ? &a.plans[s_ld(&a.tiles[tile].plan)] : nullptr;
+    auto erased_of = [&](int m) -> int { return BATCH ? s_ld(&pl->erased[m]) : a.erased[m]; };
+    const int my_erased = wave < S::kM ? erased_of(wave) : 0;
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
     {
       if (wave < S::kM) {
@@ -371,7 +392,7 @@ void k_restore_syn(SynRestoreArgs a) {
         uint32_t Pl[16];
 #pragma unroll
         for (int b = 0; b < 16; ++b) Pl[b] = W[b ^ 8];
-        syn_put_point(L, BATCH ? a.objs[o].point[wave * S::kLoadPer + s] : a.point[wave * S::kLoadPer + s], Pl);
+        syn_put_point(L, BATCH ? s_ld(&pl->point[wave * S::kLoadPer + s]) : a.point[wave * S::kLoadPer + s], Pl);
       }
     }
     st.mark(0);
@@ -407,7 +428,7 @@ void k_restore_syn(SynRestoreArgs a) {
           const Plane16 t1 = plane_mulx(tt);
 #pragma unroll
           for (int m = 0; m < kMC; ++m) {
-            const uint32_t sel = BATCH ? a.plans[a.objs[o].plan].solve_sel[m0 + m][b >> 2] : a.solve_sel[m0 + m][b >> 2];
+            const uint32_t sel = BATCH ? s_ld(&pl->solve_sel[m0 + m][b >> 2]) : a.solve_sel[m0 + m][b >> 2];
             const uint32_t two = (sel >> (8 * (b & 3) + wave)) & 0x101u;
             if (two == 1u)
               ce[m] = plane_xor(ce[m], tt);
@@ -424,7 +445,7 @@ void k_restore_syn(SynRestoreArgs a) {
 #pragma unroll
         for (int m = 0; m < kMC; ++m) {
           __attribute__((address_space(3))) uint64_t *dst =
-              (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * erased_of(o, m0 + m));
+              (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * erased_of(m0 + m));
 #pragma unroll
           for (int h = 0; h < 8; ++h)
             __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1),
@@ -441,22 +462,52 @@ void k_restore_syn(SynRestoreArgs a) {
       // (P(e_w) stripe by stripe).  Undo the stage-1 transpose and store it as
       // big-endian cells, one 1 KiB store per wave-instruction; no
       // interpolation (fused "decode + re-encode" of sync_process.cpp:313-335).
-      uint8_t *const rg = wave < S::kM ? (BATCH ? a.objs[o].regen[wave] : a.regen[wave]) : nullptr;
+      if constexpr (BATCH) {
+        if (wave < S::kM) {
+          uint32_t Pl[16], W[16];
+          syn_get_point(L, my_erased, Pl);
+#pragma unroll
+          for (int b = 0; b < 16; ++b) W[b ^ 8] = Pl[b];
+          transpose16x2(W, bm);  // self-inverse: back to the loaded word layout
+          const uint32_t trailer = s_ld(&a.tiles[tile].trailer);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const SynBatchObj &d = half_obj(tile, h);
+            uint8_t *const rg = s_ld(&d.regen[wave]);
+            if (rg == nullptr) continue;
+            const uint64_t st0 = half_s0(tile, h);
+            const uint64_t clen = s_ld(&d.chunk_len);
+            // the T cells; the trailer cell is copied from survivor 0 by the
+            // object's last half (as restore + re-encode writes it)
+            const int64_t valid = (int64_t)clen - 2 - (int64_t)(2 * st0);
+            uint8_t *dst = rg + 2 * st0 + 16 * lane;
+            if (valid >= 2 * (int64_t)kHalfStripes) {
+#pragma unroll
+              for (int q = 0; q < 2; ++q)
+                g_st<8>(dst + 1024 * q, u32x4{W[8 * h + 4 * q], W[8 * h + 4 * q + 1], W[8 * h + 4 * q + 2],
+                                              W[8 * h + 4 * q + 3]});
+            } else {
+#pragma unroll
+              for (int q = 0; q < 2; ++q)
+                st16_guard(dst + 1024 * q,
+                           u32x4{W[8 * h + 4 * q], W[8 * h + 4 * q + 1], W[8 * h + 4 * q + 2], W[8 * h + 4 * q + 3]},
+                           valid - 16 * lane - 1024 * q);
+            }
+            if (((trailer >> h) & 1u) && lane == 0)
+              *(gmem<uint16_t> *)(rg + clen - 2) = *(const gmem<uint16_t> *)(s_ld(&d.chunks[0]) + clen - 2);
+          }
+        }
+        __syncthreads();  // every wave is done with this tile's planes
+        continue;
+      }
+      uint8_t *const rg = wave < S::kM ? a.regen[wave] : nullptr;
       if (rg != nullptr) {
         uint32_t Pl[16], W[16];
         syn_get_point(L, my_erased, Pl);
 #pragma unroll
         for (int b = 0; b < 16; ++b) W[b ^ 8] = Pl[b];
         transpose16x2(W, bm);  // self-inverse: back to the loaded word layout
-        if constexpr (BATCH) {
-          // the whole replica, trailer included: every survivor holds the
-          // trailer value p at cell T, so the recovered cell T is p as well
-          uint8_t *dst = rg + 2 * stripe0 + 16 * lane;
-          const int64_t valid = (int64_t)(a.objs[o].chunk_len - 2 * stripe0) - 16 * lane;
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            st16_guard(dst + 1024 * q, u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]}, valid - 1024 * q);
-        } else {
+        {
           uint8_t *dst = rg + (uint64_t)o * a.regen_stride + 2 * stripe0 + 16 * lane;
 #pragma unroll
           for (int q = 0; q < 4; ++q)
@@ -471,9 +522,32 @@ void k_restore_syn(SynRestoreArgs a) {
       uint32_t cells[16 * S::kCells];
       syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
       if (kLateLoad && !BATCH) prefetch(tile + t_step);
-      uint8_t *dst = BATCH ? a.objs[o].out : a.out + (uint64_t)o * a.out_stride;
-      // batch: bytes of this tile's output still inside the object's E bytes
-      const int64_t out_valid = BATCH ? (int64_t)a.objs[o].out_len - (int64_t)(stripe0 * (2 * K)) : INT64_MAX;
+      // this wave's copy-out: 1024 kChunks bytes at wofs of the tile's output
+      // (batch: of its half's object's output, with out_valid bytes of the
+      // object still to go from there)
+      constexpr int kChunks = 4 * K / WV;  // 1 KiB pieces of the tile (2048 stripes x 2K bytes) each wave writes
+      constexpr uint32_t kHalfBytes = kHalfStripes * 2 * K;
+      static_assert(kHalfBytes % (1024u * kChunks) == 0, "a wave's copy-out lies in one half");
+      // (computed where the stores start: live across the staging, the
+      // addresses cost k = 32 SGPR spills)
+      struct Target {
+        uint8_t *g0;
+        int64_t valid;
+        bool guard;
+      };
+      auto target = [&]() -> Target {
+        const uint32_t wofs = 1024u * kChunks * wave;
+        if constexpr (BATCH) {
+          const int h = (int)(wofs / kHalfBytes);
+          const SynBatchObj &d = half_obj(tile, h);
+          const uint64_t at = half_s0(tile, h) * (2 * K) + (wofs - h * kHalfBytes);
+          const int64_t valid = (int64_t)s_ld(&d.out_len) - (int64_t)at;
+          return {s_ld(&d.out) + at + 16u * lane, valid, valid < 1024 * kChunks};
+        } else {
+          return {a.out + (uint64_t)o * a.out_stride + stripe0 * (2 * K) + wofs + 16u * lane,
+                  INT64_MAX, false};
+        }
+      };
       constexpr int kGroups = S::kCells / 2;  // word groups (2 cells) per wave
       if constexpr (K == 16) {
         // Stage the tile's output in LDS (the planes are dead once every wave
@@ -514,19 +588,20 @@ void k_restore_syn(SynRestoreArgs a) {
         st.mark(16);
         // 16-byte chunk c = 64 (kChunks wave + i) + lane of the tile: stripe c/2,
         // half c%2, at 16 c + 8 (c / 16) = r0 + 1056 i
-        constexpr int kChunks = 64 / WV;  // 1 KiB pieces of the tile each wave writes
         const lds_char *r0 = L.base + 1056u * kChunks * wave + 16u * lane + 8u * (lane >> 4);
-        uint8_t *g0 = dst + stripe0 * (2 * K) + 1024u * kChunks * wave + 16u * lane;
-#pragma unroll
-        for (int i = 0; i < kChunks; ++i) {
+        const auto [g0, out_valid, guard] = target();
+        auto piece = [&](int i) {
           const lds_char *r = r0 + 1056 * i;
           const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
           const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
-          if constexpr (BATCH)
-            st16_guard(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]},
-                       out_valid - (int64_t)(1024u * kChunks * wave + 16u * lane + 1024 * i));
-          else
-            g_st<8>(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]});
+          return u32x4{v0[0], v0[1], v1[0], v1[1]};
+        };
+        if (!guard) {
+#pragma unroll
+          for (int i = 0; i < kChunks; ++i) g_st<8>(g0 + 1024 * i, piece(i));
+        } else {
+#pragma unroll
+          for (int i = 0; i < kChunks; ++i) st16_guard(g0 + 1024 * i, piece(i), out_valid - 16 * lane - 1024 * i);
         }
         st.mark(17);
       } else {
@@ -564,18 +639,21 @@ void k_restore_syn(SynRestoreArgs a) {
         // 16-byte chunk c = 64 (16 wave + i) + lane of the tile: stripe c/4,
         // quarter c%4, at 64 (c/4) + 8 (c/32) + 16 (c%4) = r0 + 1040 i (one
         // per-lane base, compile-time offsets: no hoisted address per i)
-        uint8_t *g0 = dst + stripe0 * (2 * K) + 16384u * wave + 16u * lane;
+        static_assert(kChunks == 16, "16 KiB of copy-out per wave");
         const lds_char *r0 = L.base + 16640u * wave + 64u * (lane >> 2) + 8u * (lane >> 5) + 16u * (lane & 3);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        const auto [g0, out_valid, guard] = target();
+        auto piece = [&](int i) {
           const lds_char *r = r0 + 1040 * i;
           const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
           const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
-          if constexpr (BATCH)
-            st16_guard(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]},
-                       out_valid - (int64_t)(16384u * wave + 16u * lane + 1024 * i));
-          else
-            g_st<8>(g0 + 1024 * i, u32x4{v0[0], v0[1], v1[0], v1[1]});
+          return u32x4{v0[0], v0[1], v1[0], v1[1]};
+        };
+        if (!guard) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) g_st<8>(g0 + 1024 * i, piece(i));
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) st16_guard(g0 + 1024 * i, piece(i), out_valid - 16 * lane - 1024 * i);
         }
         st.mark(17);
       }

@@ -20,6 +20,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "ec_internal.hpp"
@@ -47,6 +48,40 @@ int device_ready() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return VDS_EC_ENODEV;
   return VDS_EC_OK;
+}
+
+// ------------------------------------------------- host field arithmetic
+// log / antilog tables for the host's k x k and M x M work (gf.h:193-253's
+// tables; the kernels never use them).  Built once, 384 KiB.
+struct Gf16Tables {
+  uint16_t log[65536];
+  uint16_t exp[2 * 65535];
+  Gf16Tables() {
+    uint32_t v = 1;
+    for (uint32_t l = 0; l < 65535; ++l) {
+      exp[l] = exp[l + 65535] = (uint16_t)v;
+      log[v] = (uint16_t)l;
+      v = gf16_mul(v, 2);
+    }
+    log[0] = 0;
+  }
+};
+
+const Gf16Tables &gf16_tables() {
+  static const Gf16Tables *t = new Gf16Tables();  // never freed
+  return *t;
+}
+
+inline uint32_t gf16_mul_fast(uint32_t a, uint32_t b) {
+  if (!a || !b) return 0;
+  const Gf16Tables &t = gf16_tables();
+  return t.exp[t.log[a] + t.log[b]];
+}
+
+inline uint32_t gf16_inv_fast(uint32_t a) {
+  if (!a) return 0;
+  const Gf16Tables &t = gf16_tables();
+  return t.exp[65535 - t.log[a]];
 }
 
 // ---------------------------------------------------------------- inverse
@@ -77,8 +112,8 @@ int lagrange_inverse(uint32_t k, const uint32_t *a, uint16_t *out, Mul mul, Inv 
 int inverse16(uint32_t k, const uint16_t *nodes, uint16_t *out) {
   std::vector<uint32_t> a(nodes, nodes + k);
   return lagrange_inverse(
-      k, a.data(), out, [](uint32_t x, uint32_t y) { return (uint32_t)gf16_mul(x, y); },
-      [](uint32_t x) { return (uint32_t)gf16_inv(x); });
+      k, a.data(), out, [](uint32_t x, uint32_t y) { return gf16_mul_fast(x, y); },
+      [](uint32_t x) { return gf16_inv_fast(x); });
 }
 
 int inverse8(uint32_t k, const uint8_t *nodes, uint16_t *out) {
@@ -105,23 +140,33 @@ bool restore_path_override_bs() {
   return bs;
 }
 
-bool plan_restore_syn(uint32_t k, const uint16_t *nodes, SynRestoreArgs &sa, uint32_t *n_out) {
+// The syndrome kernel's point assignment for a survivor list: eligible when
+// the k ids are distinct points of 0..k+k/4-1 for a compiled (k, n); fills
+// sa.point / sa.erased and the erased set as a bitmask (the plan's key).
+bool syn_points(uint32_t k, const uint16_t *nodes, SynRestoreArgs &sa, uint32_t *n_out, uint64_t *key) {
   if (!nodes || restore_path_override_bs()) return false;
   const uint32_t n = k + k / 4;
   if (k % 4 || !has_restore_syn(k, n)) return false;
-  const uint16_t *W = restore_syn_weights(k, n);
-  const uint32_t m = n - k;
-  std::vector<bool> seen(n, false);
+  uint64_t seen = 0;
   for (uint32_t j = 0; j < k; ++j) {
-    if (nodes[j] >= n || seen[nodes[j]]) return false;
-    seen[nodes[j]] = true;
+    if (nodes[j] >= n || ((seen >> nodes[j]) & 1u)) return false;
+    seen |= 1ull << nodes[j];
     sa.point[j] = (uint8_t)nodes[j];
   }
   uint32_t e = 0;
   for (uint32_t a = 0; a < n; ++a)
-    if (!seen[a]) sa.erased[e++] = (uint8_t)a;
+    if (!((seen >> a) & 1u)) sa.erased[e++] = (uint8_t)a;
+  *n_out = n;
+  *key = ~seen & ((1ull << n) - 1);
+  return true;
+}
+
+// R = W_E^{-1} as the kernel's bit selections (sa.erased set by syn_points).
+bool syn_solve(uint32_t k, uint32_t n, SynRestoreArgs &sa) {
+  const uint16_t *W = restore_syn_weights(k, n);
+  const uint32_t m = n - k;
   // Gauss-Jordan on [W_E | I] (m <= 8)
-  std::vector<uint32_t> A((size_t)m * 2 * m, 0);
+  uint32_t A[8 * 16] = {};
   for (uint32_t j = 0; j < m; ++j) {
     for (uint32_t i = 0; i < m; ++i) A[j * 2 * m + i] = W[j * n + sa.erased[i]];
     A[j * 2 * m + m + j] = 1;
@@ -132,12 +177,12 @@ bool plan_restore_syn(uint32_t k, const uint16_t *nodes, SynRestoreArgs &sa, uin
     if (piv == m) return false;  // cannot happen for distinct points
     if (piv != c)
       for (uint32_t x = 0; x < 2 * m; ++x) std::swap(A[c * 2 * m + x], A[piv * 2 * m + x]);
-    const uint32_t iv = gf16_inv(A[c * 2 * m + c]);
-    for (uint32_t x = 0; x < 2 * m; ++x) A[c * 2 * m + x] = gf16_mul(A[c * 2 * m + x], iv);
+    const uint32_t iv = gf16_inv_fast(A[c * 2 * m + c]);
+    for (uint32_t x = 0; x < 2 * m; ++x) A[c * 2 * m + x] = gf16_mul_fast(A[c * 2 * m + x], iv);
     for (uint32_t r = 0; r < m; ++r) {
       const uint32_t f = A[r * 2 * m + c];
       if (r == c || f == 0) continue;
-      for (uint32_t x = 0; x < 2 * m; ++x) A[r * 2 * m + x] ^= gf16_mul(f, A[c * 2 * m + x]);
+      for (uint32_t x = 0; x < 2 * m; ++x) A[r * 2 * m + x] ^= gf16_mul_fast(f, A[c * 2 * m + x]);
     }
   }
   // R[i][j]: row i = the erased point the kernel's wave i recovers
@@ -148,8 +193,12 @@ bool plan_restore_syn(uint32_t k, const uint16_t *nodes, SynRestoreArgs &sa, uin
       for (uint32_t b = 0; b < 16; ++b)
         if ((r >> b) & 1u) sa.solve_sel[i][b >> 2] |= 1u << (8 * (b & 3) + j);
     }
-  *n_out = n;
   return true;
+}
+
+bool plan_restore_syn(uint32_t k, const uint16_t *nodes, SynRestoreArgs &sa, uint32_t *n_out) {
+  uint64_t key = 0;
+  return syn_points(k, nodes, sa, n_out, &key) && syn_solve(k, *n_out, sa);
 }
 
 // ---------------------------------------------------------- encode core
@@ -254,7 +303,9 @@ struct ParamSlot {
   uint8_t *h = nullptr, *d = nullptr;
   size_t cap = 0;
   hipEvent_t ev = nullptr;
-  bool pending = false;
+  hipEvent_t copied = nullptr;  // the host -> device copy on the ring's copy stream
+  bool pending = false;  // its event guards the device copy's readers
+  bool busy = false;     // acquired, not yet released
 };
 
 struct ParamRing {
@@ -262,6 +313,7 @@ struct ParamRing {
   std::mutex mu;
   ParamSlot slot[kSlots];
   unsigned next = 0;
+  hipStream_t copy = nullptr;  // the copies run here, beside the caller's kernels
 };
 
 ParamRing *param_ring() {
@@ -275,34 +327,63 @@ ParamRing *param_ring() {
   return rings[dev];
 }
 
-// Stage `bytes` from blob into a device slot on stream s; *dev receives the
-// device address.  Call param_release(slot, s) after the launches reading it.
-hipError_t param_stage(const std::vector<uint8_t> &blob, hipStream_t s, const uint8_t **dev, ParamSlot **out) {
+// A slot of at least `bytes` whose host side the caller may write (sl->h);
+// then param_commit copies it to the device on the caller's stream, and
+// param_release after the launches reading it.  A slot stays reserved
+// (busy) from acquire to release, so threads sharing the ring never write
+// one another's.
+hipError_t param_acquire(size_t bytes, ParamSlot **out) {
+  *out = nullptr;
   ParamRing *r = param_ring();
   if (!r) return hipErrorNoDevice;
   std::lock_guard<std::mutex> g(r->mu);
-  ParamSlot &sl = r->slot[r->next++ % ParamRing::kSlots];
+  // first choice: an idle slot already big enough whose readers are done
+  // (no allocation, no wait); else the next idle slot in rotation
+  ParamSlot *sp = nullptr;
+  for (int i = 0; i < ParamRing::kSlots && !sp; ++i) {
+    ParamSlot &c = r->slot[(r->next + i) % ParamRing::kSlots];
+    if (!c.busy && c.cap >= bytes && (!c.pending || hipEventQuery(c.ev) == hipSuccess)) sp = &c;
+  }
+  for (int i = 0; i < ParamRing::kSlots && !sp; ++i) {
+    ParamSlot &c = r->slot[r->next++ % ParamRing::kSlots];
+    if (!c.busy) sp = &c;
+  }
+  if (!sp) return hipErrorOutOfMemory;  // kSlots acquisitions in flight at once
   hipError_t e = hipSuccess;
+  if (!r->copy && (e = hipStreamCreateWithFlags(&r->copy, hipStreamNonBlocking)) != hipSuccess) return e;
+  ParamSlot &sl = *sp;
   if (sl.pending) {
     e = hipEventSynchronize(sl.ev);
     sl.pending = false;
     if (e != hipSuccess) return e;
   }
   if (!sl.ev && (e = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming)) != hipSuccess) return e;
-  if (blob.size() > sl.cap) {
+  if (!sl.copied && (e = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming)) != hipSuccess) return e;
+  if (bytes > sl.cap) {
     if (sl.h) (void)hipHostFree(sl.h);
     if (sl.d) (void)hipFree(sl.d);
     sl.h = sl.d = nullptr;
     sl.cap = 0;
-    if ((e = hipHostMalloc(&sl.h, blob.size(), 0)) != hipSuccess) return e;
-    if ((e = hipMalloc(&sl.d, blob.size())) != hipSuccess) return e;
-    sl.cap = blob.size();
+    if ((e = hipHostMalloc(&sl.h, bytes, 0)) != hipSuccess) return e;
+    if ((e = hipMalloc(&sl.d, bytes)) != hipSuccess) return e;
+    sl.cap = bytes;
   }
-  std::memcpy(sl.h, blob.data(), blob.size());
-  if ((e = hipMemcpyAsync(sl.d, sl.h, blob.size(), hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-  *dev = sl.d;
+  sl.busy = true;
   *out = &sl;
   return hipSuccess;
+}
+
+// The copy runs on the ring's copy stream and s waits for it, so the copy
+// for one call overlaps the kernels of the call before it on s.  (The slot's
+// previous readers are done: acquire waited for its event.)
+hipError_t param_commit(ParamSlot *sl, size_t bytes, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  ParamRing *r = param_ring();
+  if (!r || !r->copy) return hipErrorNoDevice;
+  hipError_t e = hipMemcpyAsync(sl->d, sl->h, bytes, hipMemcpyHostToDevice, r->copy);
+  if (e == hipSuccess) e = hipEventRecord(sl->copied, r->copy);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, sl->copied, 0);
+  return e;
 }
 
 hipError_t param_release(ParamSlot *sl, hipStream_t s) {
@@ -311,6 +392,22 @@ hipError_t param_release(ParamSlot *sl, hipStream_t s) {
   std::lock_guard<std::mutex> g(r->mu);
   const hipError_t e = hipEventRecord(sl->ev, s);
   sl->pending = e == hipSuccess;
+  sl->busy = false;
+  return e;
+}
+
+// Stage blob into a device slot on stream s; *dev receives the device
+// address.  Call param_release(slot, s) after the launches reading it.
+hipError_t param_stage(const std::vector<uint8_t> &blob, hipStream_t s, const uint8_t **dev, ParamSlot **out) {
+  hipError_t e = param_acquire(blob.size(), out);
+  if (e != hipSuccess) return e;
+  std::memcpy((*out)->h, blob.data(), blob.size());
+  *dev = (*out)->d;
+  e = param_commit(*out, blob.size(), s);
+  if (e != hipSuccess) {
+    (void)param_release(*out, s);
+    *out = nullptr;
+  }
   return e;
 }
 
@@ -834,50 +931,180 @@ int check_restore_args(uint32_t k, const Id *nodes, const uint8_t *const *chunks
 // replicas found PER OBJECT, dht_network_client.cpp:851-901; sync_process
 // repairs object by object, sync_process.cpp:313-335).  Objects whose
 // survivors lie within the syndrome kernel's points go to ONE launch of
-// k_restore_syn in batch mode, over every tile of every such object; the
-// erasure plan (M x M solve) is computed once per distinct erased set.  Other
+// k_restore_syn in batch mode over every half-tile (kHalfStripes stripes) of
+// every such object, the halves of one erased set paired into tiles; other
 // objects fall back to one restore_device / regenerate_device call each, on
 // the same stream.  Nothing synchronises.
-struct BatchPlanCache {
-  std::vector<SynBatchPlan> plans;
-  std::vector<std::pair<uint64_t, uint32_t>> keys;  // erased-set bitmask -> plan index
-  int find_or_add(uint64_t key, const SynRestoreArgs &sa, uint32_t m) {
-    for (auto &kv : keys)
-      if (kv.first == key) return (int)kv.second;
-    SynBatchPlan p{};
-    for (uint32_t i = 0; i < m; ++i) p.erased[i] = sa.erased[i];
-    std::memcpy(p.solve_sel, sa.solve_sel, sizeof p.solve_sel);
-    plans.push_back(p);
-    keys.push_back({key, (uint32_t)plans.size() - 1});
-    return (int)plans.size() - 1;
-  }
+//
+// An erased set's plan (the M x M solve) never changes, so solved plans are
+// kept process-wide: a repair loop meets the same few loss patterns again and
+// again.  (Bounded: past kMax entries the store is cleared.)
+struct SynPlanStore {
+  static constexpr size_t kMax = 1u << 16;
+  std::mutex mu;
+  std::unordered_map<uint64_t, SynBatchPlan> map;
 };
 
-// Stage the batch tables (objects, plans, tile -> object) and launch.
-int launch_syn_batch(uint32_t k, uint32_t n, const std::vector<SynBatchObj> &objs, const BatchPlanCache &pc,
-                     const std::vector<uint32_t> &tile_obj, bool regen, hipStream_t s) {
-  if (tile_obj.empty()) return VDS_EC_OK;
-  std::vector<uint8_t> blob;
-  const size_t o_objs = blob_append(blob, objs.data(), objs.size());
-  const size_t o_plans = blob_append(blob, pc.plans.data(), pc.plans.size());
-  const size_t o_tiles = blob_append(blob, tile_obj.data(), tile_obj.size());
-  const uint8_t *d = nullptr;
-  ParamSlot *slot = nullptr;
-  hipError_t e = param_stage(blob, s, &d, &slot);
-  if (e == hipSuccess) {
-    SynRestoreArgs sa{};
-    sa.objs = reinterpret_cast<const SynBatchObj *>(d + o_objs);
-    sa.plans = reinterpret_cast<const SynBatchPlan *>(d + o_plans);
-    sa.tile_obj = reinterpret_cast<const uint32_t *>(d + o_tiles);
-    sa.total_tiles = (uint32_t)tile_obj.size();
-    e = launch_restore_syn_batch(k, n, sa, s, regen);
+SynPlanStore &syn_plan_store() {
+  static SynPlanStore *st = new SynPlanStore();  // never freed: outlives every caller
+  return *st;
+}
+
+// The plan of the erased set ~seen (k, n = k + k/4 compiled): points and
+// erased points ascending, the solve from the store or computed.
+bool syn_plan(uint32_t k, uint32_t n, uint64_t seen, SynBatchPlan *out) {
+  const uint64_t key = (~seen & ((1ull << n) - 1)) | ((uint64_t)k << 56);
+  SynPlanStore &st = syn_plan_store();
+  {
+    std::lock_guard<std::mutex> g(st.mu);
+    auto it = st.map.find(key);
+    if (it != st.map.end()) {
+      *out = it->second;
+      return true;
+    }
   }
-  if (slot) {
+  SynRestoreArgs sa{};
+  uint32_t e = 0, j = 0;
+  for (uint32_t a = 0; a < n; ++a) {
+    if ((seen >> a) & 1u)
+      sa.point[j++] = (uint8_t)a;
+    else
+      sa.erased[e++] = (uint8_t)a;
+  }
+  if (j != k || !syn_solve(k, n, sa)) return false;
+  SynBatchPlan p{};
+  std::memcpy(p.erased, sa.erased, sizeof p.erased);
+  std::memcpy(p.point, sa.point, sizeof p.point);
+  std::memcpy(p.solve_sel, sa.solve_sel, sizeof p.solve_sel);
+  std::lock_guard<std::mutex> g(st.mu);
+  if (st.map.size() >= SynPlanStore::kMax) st.map.clear();
+  st.map.emplace(key, p);
+  *out = p;
+  return true;
+}
+
+// Survivor set of one object as a bitmask over the syndrome kernel's points,
+// with pos[a] = the node-list index of point a; false when not eligible.
+inline bool syn_survivors(uint32_t k, uint32_t n, const uint16_t *nd, uint64_t *seen, uint8_t *pos) {
+  uint64_t m = 0;
+  for (uint32_t j = 0; j < k; ++j) {
+    const uint32_t a = nd[j];
+    if (a >= n || ((m >> a) & 1u)) return false;
+    m |= 1ull << a;
+    pos[a] = (uint8_t)j;
+  }
+  *seen = m;
+  return true;
+}
+
+// Host-side builder of one batched launch, written straight into a pinned
+// parameter slot: objs (and the empty object), then tiles, then plans.
+struct SynBatchBuild {
+  uint32_t k, n;
+  ParamSlot *slot = nullptr;
+  size_t cap_objs = 0, cap_tiles = 0, cap_plans = 0, o_tiles = 0, o_plans = 0;
+  SynBatchObj *objs = nullptr;
+  uint32_t nobj = 0;
+  std::vector<uint32_t> obj_plan, obj_halves;
+  std::vector<SynBatchPlan> plans;
+  // survivor set -> plans[]: open addressing, linear probing (a set is a
+  // nonzero bitmask; 0 marks a free entry)
+  std::vector<uint64_t> hkey;
+  std::vector<uint32_t> hval;
+  unsigned hshift = 64;
+
+  static size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
+
+  hipError_t begin(uint32_t count, uint64_t halves) {
+    cap_objs = (size_t)count + 1;
+    cap_tiles = (size_t)((halves + count + 1) / 2 + 1);  // pairs within each plan: <= (halves + plans) / 2
+    cap_plans = count;
+    o_tiles = up16(cap_objs * sizeof(SynBatchObj));
+    o_plans = up16(o_tiles + cap_tiles * sizeof(SynBatchTile));
+    hipError_t e = param_acquire(o_plans + cap_plans * sizeof(SynBatchPlan), &slot);
+    if (e == hipSuccess) objs = reinterpret_cast<SynBatchObj *>(slot->h);
+    obj_plan.reserve(count);
+    obj_halves.reserve(count);
+    unsigned bits = 4;
+    while ((1ull << bits) < 2ull * count) ++bits;
+    hkey.assign(1ull << bits, 0);
+    hval.assign(1ull << bits, 0);
+    hshift = 64 - bits;
+    return e;
+  }
+  // A new object of survivor set `seen`; nullptr if the set has no solve.
+  SynBatchObj *add(uint64_t seen, const uint8_t *const *chunks, const uint8_t *pos, uint64_t halves) {
+    const size_t mask = hkey.size() - 1;
+    size_t i = (size_t)((seen * 0x9E3779B97F4A7C15ull) >> hshift);
+    while (hkey[i] != 0 && hkey[i] != seen) i = (i + 1) & mask;
+    uint32_t p;
+    if (hkey[i] == seen) {
+      p = hval[i];
+    } else {
+      SynBatchPlan pl;
+      if (!syn_plan(k, n, seen, &pl)) return nullptr;
+      p = (uint32_t)plans.size();
+      plans.push_back(pl);
+      hkey[i] = seen;
+      hval[i] = p;
+    }
+    SynBatchObj &d = objs[nobj++];
+    uint32_t j = 0;
+    for (uint64_t b = seen; b; b &= b - 1) d.chunks[j++] = chunks[pos[__builtin_ctzll(b)]];
+    obj_plan.push_back(p);
+    obj_halves.push_back((uint32_t)halves);
+    return &d;
+  }
+  // Pair the halves of each plan into tiles, stage and launch (regenerate:
+  // the last half of every object also copies its trailer cell).
+  int launch(bool regen, hipStream_t s) {
+    if (nobj == 0) {
+      const hipError_t e = param_release(slot, s);
+      return hip_status(e);
+    }
+    const uint32_t empty = nobj;
+    std::memset(&objs[empty], 0, sizeof(SynBatchObj));
+    std::vector<uint64_t> first(plans.size() + 1, 0);  // tile offset of each plan
+    std::vector<uint64_t> used(plans.size(), 0);
+    for (uint32_t o = 0; o < nobj; ++o) first[obj_plan[o] + 1] += obj_halves[o];
+    for (size_t p = 0; p < plans.size(); ++p) first[p + 1] = first[p] + (first[p + 1] + 1) / 2;
+    const uint64_t ntiles = first[plans.size()];
+    if (ntiles > cap_tiles || ntiles > 0xFFFFFFFFull) {
+      (void)param_release(slot, s);
+      return VDS_EC_EINVAL;
+    }
+    SynBatchTile *tiles = reinterpret_cast<SynBatchTile *>(slot->h + o_tiles);
+    for (uint64_t t = 0; t < ntiles; ++t) tiles[t] = SynBatchTile{{empty, empty}, {0, 0}, 0, 0, {0, 0}};
+    for (size_t p = 0; p < plans.size(); ++p)
+      for (uint64_t t = first[p]; t < first[p + 1]; ++t) tiles[t].plan = (uint32_t)p;
+    for (uint32_t o = 0; o < nobj; ++o) {
+      const uint32_t p = obj_plan[o];
+      for (uint32_t h = 0; h < obj_halves[o]; ++h) {
+        const uint64_t i = used[p]++;
+        SynBatchTile &t = tiles[first[p] + i / 2];
+        t.obj[i & 1] = o;
+        t.stripe0[i & 1] = h * kHalfStripes;
+        if (regen && h + 1 == obj_halves[o]) t.trailer |= 1u << (i & 1);
+      }
+    }
+    std::memcpy(slot->h + o_plans, plans.data(), plans.size() * sizeof(SynBatchPlan));
+    hipError_t e = param_commit(slot, o_plans + plans.size() * sizeof(SynBatchPlan), s);
+    if (e == hipSuccess) {
+      SynRestoreArgs sa{};
+      sa.objs = reinterpret_cast<const SynBatchObj *>(slot->d);
+      sa.tiles = reinterpret_cast<const SynBatchTile *>(slot->d + o_tiles);
+      sa.plans = reinterpret_cast<const SynBatchPlan *>(slot->d + o_plans);
+      sa.total_tiles = (uint32_t)ntiles;
+      e = launch_restore_syn_batch(k, n, sa, s, regen);
+    }
     const hipError_t re = param_release(slot, s);
     if (e == hipSuccess) e = re;
+    return hip_status(e);
   }
-  return hip_status(e);
-}
+  void abandon(hipStream_t s) {
+    if (slot) (void)param_release(slot, s);  // (nothing was copied from it)
+  }
+};
 
 int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
                          const uint64_t *chunk_sizes, const uint16_t *paddings, uint8_t *const *outs, unsigned flags,
@@ -886,6 +1113,7 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
   if (count == 0) return VDS_EC_OK;
   // every object is validated before anything is enqueued
   std::vector<uint64_t> lens(count);
+  uint64_t halves = 0;
   for (uint32_t o = 0; o < count; ++o) {
     int rc = check_restore_args(k, nodes + (uint64_t)o * k, chunks + (uint64_t)o * k, chunk_sizes[o]);
     if (rc) return rc;
@@ -893,44 +1121,40 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
     lens[o] = restored_len(2, k, chunk_sizes[o], paddings[o], flags, &ok);
     if (!ok) return VDS_EC_ERESTORE;
     if (lens[o] && !outs[o]) return VDS_EC_EINVAL;
+    const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);  // stripes that produce output
+    halves += (need + kHalfStripes - 1) / kHalfStripes;
   }
   int rc = device_ready();
   if (rc) return rc;
-  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
   const uint32_t n = k + k / 4;
-  std::vector<SynBatchObj> objs;
-  std::vector<uint32_t> tile_obj;
-  BatchPlanCache pc;
+  const bool syn = !(flags & VDS_EC_F_CELLS) && k % 4 == 0 && has_restore_syn(k, n) && !restore_path_override_bs();
   std::vector<uint32_t> fallback;
+  SynBatchBuild bb{k, n};
+  if (syn) {
+    hipError_t e = bb.begin(count, halves);
+    if (e != hipSuccess) return hip_status(e);
+  }
+  uint8_t pos[64];
   for (uint32_t o = 0; o < count; ++o) {
-    const uint16_t *nd = nodes + (uint64_t)o * k;
-    SynRestoreArgs sa{};
-    uint32_t syn_n = 0;
-    const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);  // stripes that produce output
-    if (cells || !plan_restore_syn(k, nd, sa, &syn_n) || syn_n != n) {
+    uint64_t seen = 0;
+    if (!syn || !syn_survivors(k, n, nodes + (uint64_t)o * k, &seen, pos)) {
       fallback.push_back(o);
       continue;
     }
+    const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);
     if (need == 0) continue;
-    uint64_t key = 0;
-    for (uint32_t i = 0; i < n - k; ++i) key |= 1ull << sa.erased[i];
-    SynBatchObj d{};
-    for (uint32_t j = 0; j < k; ++j) {
-      d.chunks[j] = chunks[(uint64_t)o * k + j];
-      d.point[j] = sa.point[j];
+    const uint64_t h = (need + kHalfStripes - 1) / kHalfStripes;
+    SynBatchObj *d = bb.add(seen, chunks + (uint64_t)o * k, pos, h);
+    if (!d) {
+      bb.abandon(s);
+      return VDS_EC_ESINGULAR;
     }
-    d.out = outs[o];
-    d.out_len = lens[o];
-    d.chunk_len = chunk_sizes[o];
-    d.plan = (uint32_t)pc.find_or_add(key, sa, n - k);
-    d.first_tile = (uint32_t)tile_obj.size();
-    const uint64_t tiles = (need + kTileStripes - 1) / kTileStripes;
-    if (tile_obj.size() + tiles > 0xFFFFFFFFull) return VDS_EC_EINVAL;
-    tile_obj.insert(tile_obj.end(), tiles, (uint32_t)objs.size());
-    objs.push_back(d);
+    d->out = outs[o];
+    std::memset(d->regen, 0, sizeof d->regen);
+    d->out_len = lens[o];
+    d->chunk_len = chunk_sizes[o];
   }
-  rc = launch_syn_batch(k, n, objs, pc, tile_obj, false, s);
-  if (rc) return rc;
+  if (syn && (rc = bb.launch(false, s))) return rc;
   for (uint32_t o : fallback) {
     if (lens[o] == 0) continue;
     std::vector<uint16_t> m((size_t)k * k);
@@ -948,56 +1172,57 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
                             hipStream_t s) {
   if (k == 0 || (count && (!nodes || !chunks || !chunk_sizes || (nt && (!targets || !outs))))) return VDS_EC_EINVAL;
   if (count == 0 || nt == 0) return VDS_EC_OK;
+  uint64_t halves = 0;
   for (uint32_t o = 0; o < count; ++o) {
     if (chunk_sizes[o] < 2 || (chunk_sizes[o] - 2) % 2) return VDS_EC_EINVAL;  // cells + BE16 trailer
     for (uint32_t j = 0; j < k; ++j)
       if (!chunks[(uint64_t)o * k + j]) return VDS_EC_EINVAL;
     for (uint32_t i = 0; i < nt; ++i)
       if (!outs[(uint64_t)o * nt + i]) return VDS_EC_EINVAL;
+    const uint64_t T = (chunk_sizes[o] - 2) / 2;
+    halves += T ? (T + kHalfStripes - 1) / kHalfStripes : 1;
   }
   int rc = device_ready();
   if (rc) return rc;
   const uint32_t n = k + k / 4;
-  std::vector<SynBatchObj> objs;
-  std::vector<uint32_t> tile_obj;
-  BatchPlanCache pc;
+  const bool syn = k % 4 == 0 && has_restore_syn(k, n) && !restore_path_override_bs();
   std::vector<uint32_t> fallback;
+  SynBatchBuild bb{k, n};
+  if (syn) {
+    hipError_t e = bb.begin(count, halves);
+    if (e != hipSuccess) return hip_status(e);
+  }
+  uint8_t pos[64];
   for (uint32_t o = 0; o < count; ++o) {
-    const uint16_t *nd = nodes + (uint64_t)o * k;
-    SynRestoreArgs sa{};
-    uint32_t syn_n = 0;
-    bool syn = plan_restore_syn(k, nd, sa, &syn_n) && syn_n == n;
-    SynBatchObj d{};
-    for (uint32_t i = 0; syn && i < nt; ++i) {  // every target must be one of the erased points
-      bool hit = false;
-      for (uint32_t w = 0; w < n - k && !hit; ++w)
-        if (sa.erased[w] == targets[(uint64_t)o * nt + i] && !d.regen[w]) {
-          d.regen[w] = outs[(uint64_t)o * nt + i];
-          hit = true;
-        }
-      syn = hit;
+    uint64_t seen = 0;
+    bool ok = syn && syn_survivors(k, n, nodes + (uint64_t)o * k, &seen, pos);
+    // every target must be an erased point, each at most once: wave w
+    // recovers the w-th erased point (ascending)
+    uint8_t *regen[kMaxFastK / 4] = {};
+    const uint64_t erased = ~seen & ((1ull << n) - 1);
+    for (uint32_t i = 0; ok && i < nt; ++i) {
+      const uint32_t t = targets[(uint64_t)o * nt + i];
+      const uint32_t w = t < n ? (uint32_t)__builtin_popcountll(erased & ((1ull << t) - 1)) : 0;
+      ok = t < n && ((erased >> t) & 1u) && !regen[w];
+      if (ok) regen[w] = outs[(uint64_t)o * nt + i];
     }
-    if (!syn) {
+    if (!ok) {
       fallback.push_back(o);
       continue;
     }
-    uint64_t key = 0;
-    for (uint32_t i = 0; i < n - k; ++i) key |= 1ull << sa.erased[i];
-    for (uint32_t j = 0; j < k; ++j) {
-      d.chunks[j] = chunks[(uint64_t)o * k + j];
-      d.point[j] = sa.point[j];
+    const uint64_t T = (chunk_sizes[o] - 2) / 2;
+    const uint64_t h = T ? (T + kHalfStripes - 1) / kHalfStripes : 1;
+    SynBatchObj *d = bb.add(seen, chunks + (uint64_t)o * k, pos, h);
+    if (!d) {
+      bb.abandon(s);
+      return VDS_EC_ESINGULAR;
     }
-    d.chunk_len = chunk_sizes[o];
-    d.plan = (uint32_t)pc.find_or_add(key, sa, n - k);
-    d.first_tile = (uint32_t)tile_obj.size();
-    const uint64_t cells_t = chunk_sizes[o] / 2;  // T cells + the trailer cell
-    const uint64_t tiles = (cells_t + kTileStripes - 1) / kTileStripes;
-    if (tile_obj.size() + tiles > 0xFFFFFFFFull) return VDS_EC_EINVAL;
-    tile_obj.insert(tile_obj.end(), tiles, (uint32_t)objs.size());
-    objs.push_back(d);
+    d->out = nullptr;
+    std::memcpy(d->regen, regen, sizeof regen);
+    d->out_len = 0;
+    d->chunk_len = chunk_sizes[o];
   }
-  rc = launch_syn_batch(k, n, objs, pc, tile_obj, true, s);
-  if (rc) return rc;
+  if (syn && (rc = bb.launch(true, s))) return rc;
   for (uint32_t o : fallback) {
     rc = regenerate_device(2, k, nodes + (uint64_t)o * k, chunks + (uint64_t)o * k, chunk_sizes[o], 0, 1,
                            targets + (uint64_t)o * nt, nt, outs + (uint64_t)o * nt, 0, s);

@@ -147,7 +147,7 @@ int vds_ec_regenerate16_batch_device(uint16_t k, uint32_t count, const uint16_t 
                                      const uint64_t *chunk_sizes, uint32_t ntargets, const uint16_t *targets,
                                      uint8_t *const *outs, void *stream);
 
-/* ---------------------------------------------------------- host entry points/* ---------------------------------------------------------- host entry points
+/* ---------------------------------------------------------- host entry points
  * Same operations on host memory (pinned staging, H2D -> kernel -> D2H on
  * the calling thread's current device).  outs: n host buffers of
  * vds_ec_replica_size(...) bytes.  This is what chunk_generator::write and

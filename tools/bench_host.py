@@ -6,7 +6,13 @@ vds_ec_restore16_host_batch (the same ring: H2D of k replicas -> restore ->
 D2H), and beside it vds_ec_restore16_host per object (ChunkStorage.restore_data).
 Prints one JSON line.  This rate is never bench.py's `value`.
 
-  python tools/bench_host.py [--objects 16] [--object-mib 64] [--k 16] [--m 4]
+  python tools/bench_host.py [--objects 16] [--object-mib 64] [--k 16] [--m 4] [--live 16384]
+
+--live N adds the production shape: N host objects of 64 KiB at k = 32, n = 64
+(dht_network.h:22-25, web/src/store/vds_api.jsx:76), encoded with one
+vds_ec_encode16_host_batch call and restored with one
+vds_ec_restore16_host_batch call from the first 32 replicas found per object
+(replica loss p = 0.02, restore_async, dht_network_client.cpp:851-901).
 """
 import argparse
 import json
@@ -25,6 +31,7 @@ p.add_argument("--object-mib", type=int, default=64)
 p.add_argument("--k", type=int, default=16)
 p.add_argument("--m", type=int, default=4)
 p.add_argument("--reps", type=int, default=2)
+p.add_argument("--live", type=int, default=0)
 a = p.parse_args()
 k, n, size = a.k, a.k + a.m, a.object_mib << 20
 rng = np.random.default_rng(1)
@@ -61,8 +68,65 @@ for _ in range(a.reps):
     best_rb = dt if best_rb is None else min(best_rb, dt)
 assert all(g.tobytes() == d.tobytes() for g, d in zip(got, objs))
 gib = a.objects * size / 2**30
+
+
+def live(count, reps):
+    """The live shape through the C ABI with flat numpy buffers (one pointer
+    per object / replica, no per-object Python arrays)."""
+    import ctypes as C
+    from vds_amd import _lib
+    lib = _lib.lib()
+    k, n, size = 32, 64, 65536
+    L = chunk.replica_size(k, size)
+    objs = rng.integers(0, 256, count * size, dtype=np.uint8)
+    reps_buf = np.ones(count * n * L, dtype=np.uint8)   # caller-owned, pre-faulted
+    out = np.ones(count * size, dtype=np.uint8)
+    obj_ptrs = (np.uint64(objs.ctypes.data) + np.arange(count, dtype=np.uint64) * np.uint64(size))
+    rep_ptrs = (np.uint64(reps_buf.ctypes.data) + np.arange(count * n, dtype=np.uint64) * np.uint64(L))
+    sizes = np.full(count, size, dtype=np.uint64)
+    ids = np.arange(n, dtype=np.uint16)
+
+    def enc():
+        _lib.check(lib.vds_ec_encode16_host_batch(k, ids.ctypes.data_as(_lib.u16p), n,
+                                                  obj_ptrs.ctypes.data_as(_lib.vpp), sizes.ctypes.data_as(_lib.u64p),
+                                                  count, rep_ptrs.ctypes.data_as(_lib.vpp), 0, 0))
+    lost = np.random.default_rng(2).random((count, n)) < 0.02
+    nodes = np.stack([np.flatnonzero(~lost[o])[:k] for o in range(count)]).astype(np.uint16)
+    chunk_ptrs = (np.uint64(reps_buf.ctypes.data) +
+                  (np.arange(count, dtype=np.uint64)[:, None] * np.uint64(n) + nodes.astype(np.uint64)) * np.uint64(L))
+    chunk_ptrs = np.ascontiguousarray(chunk_ptrs)
+    csz = np.full(count, L, dtype=np.uint64)
+    out_ptrs = (np.uint64(out.ctypes.data) + np.arange(count, dtype=np.uint64) * np.uint64(size))
+    caps = np.full(count, size, dtype=np.uint64)
+
+    def rest():
+        caps[:] = size
+        _lib.check(lib.vds_ec_restore16_host_batch(k, nodes.ctypes.data_as(_lib.u16p), chunk_ptrs.ctypes.data_as(_lib.vpp),
+                                                   csz.ctypes.data_as(_lib.u64p), count,
+                                                   out_ptrs.ctypes.data_as(_lib.vpp), caps.ctypes.data_as(_lib.u64p),
+                                                   0, 0))
+
+    def best(fn):
+        fn()
+        b = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            dt = time.perf_counter() - t0
+            b = dt if b is None else min(b, dt)
+        return b
+    te = best(enc)
+    tr = best(rest)
+    assert np.array_equal(out, objs), "live host restore differs"
+    g = count * size / 2**30
+    return {"shape": f"k=32, n=64, {count} x 64 KiB host objects, loss p=0.02", "encode_GiBps": round(g / te, 3),
+            "repair_GiBps": round(g / tr, 3), "encode_s": round(te, 4), "repair_s": round(tr, 4),
+            "pcie_bytes_per_object_encode": size + n * L, "pcie_bytes_per_object_repair": k * L + size}
+
+
 print(json.dumps({"metric": "host-resident (PCIe-inclusive) encode / repair GiB/s", "objects": a.objects,
                   "object_bytes": size, "k": k, "n": n, "erased": erased,
                   "encode_GiBps": round(gib / best_enc, 3), "repair_GiBps": round(gib / best_rb, 3),
                   "repair_per_object_GiBps": round(gib / best_rep, 3),
-                  "encode_s": round(best_enc, 4), "repair_s": round(best_rb, 4)}), flush=True)
+                  "encode_s": round(best_enc, 4), "repair_s": round(best_rb, 4),
+                  "live": live(a.live, a.reps) if a.live else None}), flush=True)

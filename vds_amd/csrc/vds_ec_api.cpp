@@ -1232,16 +1232,62 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
 }
 
 // ------------------------------------------------- multi-GPU host batch
-// Pinned staging of the host batch path, one ring per device, created on
-// first use and kept (like HostCtx): hipHostMalloc of hundreds of MiB costs
-// more than the encode it feeds.
+// Host-resident objects, many per launch: runs of consecutive objects of one
+// size are packed into groups of up to kGroupBytes of input, and the groups
+// go round-robin to the devices (one host thread each).  Per device a ring of
+// kSlots pinned slots keeps the host copies of one group (gathered into, or
+// scattered out of, pinned staging by a few threads), the DMA of another and
+// the kernels of a third in flight together.  Staging is kept across calls:
+// hipHostMalloc of hundreds of MiB costs more than the encode it feeds.
+// The bound is PCIe: input + every replica cross it, and on the MI355X box
+// its two directions together carry about one direction's 57 GB/s
+// (tools/ubench/pcie.py).
+constexpr uint64_t kGroupBytes = 64ull << 20;
+
+struct Copy {
+  uint8_t *dst;
+  const uint8_t *src;
+  size_t len;
+};
+
+// The copies, split over up to 8 threads by bytes: one thread's memcpy into
+// pinned memory runs far below host memory bandwidth (28 vs 113 GB/s with 8).
+void parallel_copy(const std::vector<Copy> &parts) {
+  size_t total = 0;
+  for (const Copy &c : parts) total += c.len;
+  const size_t kMinPerThread = 8u << 20;
+  size_t nt = std::min<size_t>(total / kMinPerThread, 8);
+  if (nt <= 1) {
+    for (const Copy &c : parts) std::memcpy(c.dst, c.src, c.len);
+    return;
+  }
+  // thread t copies bytes [total t / nt, total (t+1) / nt) of the concatenation
+  auto run = [&](size_t t) {
+    const size_t lo = total * t / nt, hi = total * (t + 1) / nt;
+    size_t at = 0;
+    for (const Copy &c : parts) {
+      const size_t b = std::max(lo, at), e = std::min(hi, at + c.len);
+      if (b < e) std::memcpy(c.dst + (b - at), c.src + (b - at), e - b);
+      at += c.len;
+      if (at >= hi) break;
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; ++t) th.emplace_back(run, t);
+  run(0);
+  for (auto &t : th) t.join();
+}
+
 struct BatchSlot {
   hipStream_t stream = nullptr;
   uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
   size_t in_cap = 0, out_cap = 0;
-  int64_t obj = -1;
+  bool busy = false;
+  std::vector<Copy> out_parts;  // the scatter of h_out once the stream is done
   int reserve(size_t in_b, size_t out_b) {
     if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VDS_EC_ENODEV;
+    in_b = std::max<size_t>(in_b, 1);
+    out_b = std::max<size_t>(out_b, 1);
     if (in_b > in_cap) {
       if (h_in) (void)hipHostFree(h_in);
       if (d_in) (void)hipFree(d_in);
@@ -1261,11 +1307,22 @@ struct BatchSlot {
     }
     return VDS_EC_OK;
   }
+  // wait for the slot's group and copy its results out
+  int drain() {
+    if (!busy) return VDS_EC_OK;
+    busy = false;
+    hipError_t e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hip_status(e);
+    parallel_copy(out_parts);
+    out_parts.clear();
+    return VDS_EC_OK;
+  }
 };
 
 struct BatchRing {
+  static constexpr int kSlots = 3;
   std::mutex mu;  // one batch call per device at a time
-  BatchSlot slot[2];
+  BatchSlot slot[kSlots];
 };
 
 BatchRing *batch_ring(int dev) {
@@ -1278,31 +1335,179 @@ BatchRing *batch_ring(int dev) {
   return rings[dev];
 }
 
-// Host copies of (dst, src) pairs of `bytes` each, split over a few threads:
-// one thread's memcpy into pinned memory runs far below host memory bandwidth.
-void parallel_copy(const std::vector<std::pair<uint8_t *, const uint8_t *>> &parts, size_t bytes) {
-  const size_t total = parts.size() * bytes;
-  const size_t kMinPerThread = 8u << 20;
-  size_t nt = total / kMinPerThread;
-  if (nt > 8) nt = 8;
-  if (nt <= 1) {
-    for (auto &p : parts) std::memcpy(p.first, p.second, bytes);
-    return;
+struct Group {
+  uint32_t o0, cnt;
+};
+
+// Runs of consecutive objects with equal key(o), at most kGroupBytes of
+// bytes(o) each (and at least one object).
+template <typename Key, typename Bytes>
+std::vector<Group> make_groups(uint32_t count, Key key, Bytes bytes) {
+  std::vector<Group> g;
+  uint64_t acc = 0;
+  for (uint32_t o = 0; o < count; ++o) {
+    const uint64_t b = bytes(o);
+    if (!g.empty() && key(o) == key(g.back().o0) && acc + b <= kGroupBytes) {
+      ++g.back().cnt;
+      acc += b;
+    } else {
+      g.push_back({o, 1});
+      acc = b;
+    }
   }
-  // split the concatenation of all parts into nt equal ranges
-  auto run = [&](size_t t) {
-    size_t lo = total * t / nt, hi = total * (t + 1) / nt;
-    while (lo < hi) {
-      const size_t pi = lo / bytes, off = lo % bytes;
-      const size_t len = std::min(bytes - off, hi - lo);
-      std::memcpy(parts[pi].first + off, parts[pi].second + off, len);
-      lo += len;
+  return g;
+}
+
+// Run enqueue(slot, group) for the groups of each device on its ring; a slot
+// is drained before it is refilled and every slot at the end.
+template <typename Enqueue>
+int run_host_batch(const std::vector<Group> &groups, int ndev, Enqueue enqueue) {
+  std::atomic<int> status{VDS_EC_OK};
+  auto worker = [&](int dev) {
+    if (hipSetDevice(dev) != hipSuccess) {
+      status = VDS_EC_ENODEV;
+      return;
+    }
+    BatchRing *ring = batch_ring(dev);
+    if (!ring) {
+      status = VDS_EC_ENODEV;
+      return;
+    }
+    std::lock_guard<std::mutex> hold(ring->mu);
+    int si = 0;
+    for (size_t g = dev; g < groups.size() && status.load() == VDS_EC_OK; g += ndev) {
+      BatchSlot &s = ring->slot[si];
+      si = (si + 1) % BatchRing::kSlots;
+      int rc = s.drain();
+      if (rc == VDS_EC_OK) {
+        rc = enqueue(s, groups[g]);
+        s.busy = true;  // (on failure too: whatever was enqueued is waited for, nothing copied out)
+        if (rc) s.out_parts.clear();
+      }
+      if (rc) {
+        status = rc;
+        break;
+      }
+    }
+    for (auto &s : ring->slot) {
+      const int rc = s.drain();
+      if (rc && status.load() == VDS_EC_OK) status = rc;
+      s.out_parts.clear();
     }
   };
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < nt; ++t) th.emplace_back(run, t);
-  run(0);
-  for (auto &t : th) t.join();
+  std::vector<std::thread> threads;
+  for (int d = 0; d < ndev && (size_t)d < groups.size(); ++d) threads.emplace_back(worker, d);
+  for (auto &t : threads) t.join();
+  return status.load();
+}
+
+int batch_devices(int max_devices, int *ndev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return VDS_EC_ENODEV;
+  if (max_devices > 0 && max_devices < n) n = max_devices;
+  *ndev = n;
+  return VDS_EC_OK;
+}
+
+int encode_host_batch(uint32_t k, const uint16_t *replicas, uint32_t n, const uint8_t *const *objs,
+                      const uint64_t *sizes, uint32_t count, uint8_t *const *outs, unsigned flags, int max_devices) {
+  if (k == 0 || (count && (!objs || !sizes || !outs)) || (n && !replicas)) return VDS_EC_EINVAL;
+  int ndev = 0;
+  int rc = batch_devices(max_devices, &ndev);
+  if (rc) return rc;
+  if (count == 0 || n == 0) return VDS_EC_OK;
+  for (uint32_t o = 0; o < count; ++o) {
+    if (sizes[o] && !objs[o]) return VDS_EC_EINVAL;
+    for (uint32_t i = 0; i < n; ++i)
+      if (!outs[(uint64_t)o * n + i]) return VDS_EC_EINVAL;
+  }
+  const std::vector<Group> groups = make_groups(
+      count, [&](uint32_t o) { return sizes[o]; },
+      [&](uint32_t o) { return sizes[o] + (uint64_t)n * vds_ec_replica_size(2, k, sizes[o], flags); });
+  return run_host_batch(groups, ndev, [&](BatchSlot &s, const Group &g) -> int {
+    const uint64_t size = sizes[g.o0], L = vds_ec_replica_size(2, k, size, flags), m = g.cnt;
+    int rc = s.reserve(m * size, m * n * L);
+    if (rc) return rc;
+    std::vector<Copy> in(m);
+    for (uint64_t o = 0; o < m; ++o) in[o] = {s.h_in + o * size, objs[g.o0 + o], size};
+    parallel_copy(in);
+    hipError_t e = size ? hipMemcpyAsync(s.d_in, s.h_in, m * size, hipMemcpyHostToDevice, s.stream) : hipSuccess;
+    if (e != hipSuccess) return hip_status(e);
+    // replica i of the group's object o at d_out + (i m + o) L
+    std::vector<uint8_t *> douts(n);
+    for (uint32_t i = 0; i < n; ++i) douts[i] = s.d_out + (uint64_t)i * m * L;
+    rc = encode_device(2, k, replicas, n, s.d_in, size, size, (uint32_t)m, douts.data(), L, flags, s.stream);
+    if (rc) return rc;
+    e = hipMemcpyAsync(s.h_out, s.d_out, m * n * L, hipMemcpyDeviceToHost, s.stream);
+    if (e != hipSuccess) return hip_status(e);
+    s.out_parts.resize(m * n);
+    for (uint64_t o = 0; o < m; ++o)
+      for (uint32_t i = 0; i < n; ++i)
+        s.out_parts[o * n + i] = {outs[(g.o0 + o) * n + i], s.h_out + (i * m + o) * L, L};
+    return VDS_EC_OK;
+  });
+}
+
+int restore_host_batch(uint32_t k, const uint16_t *nodes, const uint8_t *const *chunks, const uint64_t *chunk_sizes,
+                       uint32_t count, uint8_t *const *outs, uint64_t *out_sizes, unsigned flags, int max_devices) {
+  if (k == 0 || (count && (!nodes || !chunks || !chunk_sizes || !outs || !out_sizes))) return VDS_EC_EINVAL;
+  int ndev = 0;
+  int rc = batch_devices(max_devices, &ndev);
+  if (rc) return rc;
+  if (count == 0) return VDS_EC_OK;
+  // Validate every object before any transfer, as restore16_host does per
+  // object (chunk.h:415-419 lengths; the trailer of the first chunk), so a
+  // bad object fails the call without partial output.
+  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
+  std::vector<uint64_t> lens(count);
+  std::vector<uint16_t> pads(count);
+  for (uint32_t o = 0; o < count; ++o) {
+    const uint64_t cs = chunk_sizes[o];
+    rc = check_restore_args(k, nodes + (uint64_t)o * k, chunks + (uint64_t)o * k, cs);
+    if (rc) return rc;
+    const uint8_t *c0 = chunks[(uint64_t)o * k];
+    pads[o] = (cells || cs < 2) ? 0 : (uint16_t)((c0[cs - 2] << 8) | c0[cs - 1]);
+    bool ok = true;
+    lens[o] = restored_len(2, k, cs, pads[o], flags, &ok);
+    if (!ok) return VDS_EC_ERESTORE;
+    if (lens[o] > out_sizes[o] || (lens[o] && !outs[o])) return VDS_EC_EINVAL;
+  }
+  // the most a group's object can restore to: (chunk_size - 2) k plus a
+  // corrupt trailer's excess, bounded by restored_len's own checks
+  const std::vector<Group> groups = make_groups(
+      count, [&](uint32_t o) { return chunk_sizes[o]; }, [&](uint32_t o) { return chunk_sizes[o] * (k + 1); });
+  rc = run_host_batch(groups, ndev, [&](BatchSlot &s, const Group &g) -> int {
+    const uint64_t cs = chunk_sizes[g.o0], m = g.cnt;
+    uint64_t cap = 1;
+    for (uint64_t o = 0; o < m; ++o) cap = std::max(cap, lens[g.o0 + o]);
+    int rc = s.reserve(m * k * cs, m * cap);
+    if (rc) return rc;
+    std::vector<Copy> in(m * k);
+    std::vector<const uint8_t *> dchunks(m * k);
+    for (uint64_t o = 0; o < m; ++o)
+      for (uint32_t j = 0; j < k; ++j) {
+        in[o * k + j] = {s.h_in + (o * k + j) * cs, chunks[(g.o0 + o) * k + j], cs};
+        dchunks[o * k + j] = s.d_in + (o * k + j) * cs;
+      }
+    parallel_copy(in);
+    hipError_t e = cs ? hipMemcpyAsync(s.d_in, s.h_in, m * k * cs, hipMemcpyHostToDevice, s.stream) : hipSuccess;
+    if (e != hipSuccess) return hip_status(e);
+    std::vector<uint64_t> csz(m, cs);
+    std::vector<uint8_t *> douts(m);
+    for (uint64_t o = 0; o < m; ++o) douts[o] = s.d_out + o * cap;
+    rc = restore_batch_device(k, (uint32_t)m, nodes + (uint64_t)g.o0 * k, dchunks.data(), csz.data(),
+                              pads.data() + g.o0, douts.data(), flags, s.stream);
+    if (rc) return rc;
+    e = hipMemcpyAsync(s.h_out, s.d_out, m * cap, hipMemcpyDeviceToHost, s.stream);
+    if (e != hipSuccess) return hip_status(e);
+    s.out_parts.clear();
+    for (uint64_t o = 0; o < m; ++o)
+      if (lens[g.o0 + o]) s.out_parts.push_back({outs[g.o0 + o], s.h_out + o * cap, lens[g.o0 + o]});
+    return VDS_EC_OK;
+  });
+  if (rc == VDS_EC_OK)
+    for (uint32_t o = 0; o < count; ++o) out_sizes[o] = lens[o];
+  return rc;
 }
 
 }  // namespace
@@ -1510,154 +1715,13 @@ int vds_ec_restore8_host(uint8_t k, const uint8_t *nodes, const uint8_t *const *
 int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,
                                const uint8_t *const *objs, const uint64_t *sizes, uint32_t count,
                                uint8_t *const *outs, unsigned flags, int max_devices) {
-  if (k == 0 || (count && (!objs || !sizes || !outs)) || (n && !replicas)) return VDS_EC_EINVAL;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VDS_EC_ENODEV;
-  if (max_devices > 0 && max_devices < ndev) ndev = max_devices;
-  if (count == 0 || n == 0) return VDS_EC_OK;
-  std::atomic<int> status{VDS_EC_OK};
-  auto worker = [&](int dev) {
-    if (hipSetDevice(dev) != hipSuccess) {
-      status = VDS_EC_ENODEV;
-      return;
-    }
-    // Two slots per device (persistent across calls): while one slot's
-    // object is on the GPU, the other's pinned staging is filled / drained.
-    BatchRing *ring = batch_ring(dev);
-    if (!ring) {
-      status = VDS_EC_ENODEV;
-      return;
-    }
-    std::lock_guard<std::mutex> hold(ring->mu);
-    auto drain = [&](BatchSlot &s) -> int {
-      if (s.obj < 0) return VDS_EC_OK;
-      hipError_t e = hipStreamSynchronize(s.stream);
-      if (e != hipSuccess) return hip_status(e);
-      const uint64_t L = vds_ec_replica_size(2, k, sizes[s.obj], flags);
-      std::vector<std::pair<uint8_t *, const uint8_t *>> parts(n);
-      for (uint32_t i = 0; i < n; ++i) parts[i] = {outs[(uint64_t)s.obj * n + i], s.h_out + i * L};
-      parallel_copy(parts, L);
-      s.obj = -1;
-      return VDS_EC_OK;
-    };
-    int si = 0;
-    for (int64_t o = dev; o < (int64_t)count && status.load() == VDS_EC_OK; o += ndev, si ^= 1) {
-      BatchSlot &s = ring->slot[si];
-      int rc = drain(s);
-      if (rc) { status = rc; break; }
-      const uint64_t size = sizes[o];
-      const uint64_t L = vds_ec_replica_size(2, k, size, flags);
-      rc = s.reserve(size ? size : 1, L * n ? L * n : 1);
-      if (rc) { status = rc; break; }
-      if (size) parallel_copy({{s.h_in, objs[o]}}, size);
-      hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, size, hipMemcpyHostToDevice, s.stream);
-      if (e != hipSuccess) { status = hip_status(e); break; }
-      std::vector<uint8_t *> douts(n);
-      for (uint32_t i = 0; i < n; ++i) douts[i] = s.d_out + (uint64_t)i * L;
-      rc = encode_device(2, k, replicas, n, s.d_in, size, size, 1, douts.data(), 0, flags, s.stream);
-      if (rc) { status = rc; break; }
-      e = hipMemcpyAsync(s.h_out, s.d_out, L * n, hipMemcpyDeviceToHost, s.stream);
-      if (e != hipSuccess) { status = hip_status(e); break; }
-      s.obj = o;
-    }
-    for (auto &s : ring->slot) {
-      int rc = drain(s);
-      if (rc && status.load() == VDS_EC_OK) status = rc;
-      s.obj = -1;
-    }
-  };
-  std::vector<std::thread> threads;
-  for (int d = 0; d < ndev; ++d) threads.emplace_back(worker, d);
-  for (auto &t : threads) t.join();
-  return status.load();
+  return encode_host_batch(k, replicas, n, objs, sizes, count, outs, flags, max_devices);
 }
 
 int vds_ec_restore16_host_batch(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks,
                                 const uint64_t *chunk_sizes, uint32_t count, uint8_t *const *outs, uint64_t *out_sizes,
                                 unsigned flags, int max_devices) {
-  if (k == 0 || (count && (!nodes || !chunks || !chunk_sizes || !outs || !out_sizes))) return VDS_EC_EINVAL;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VDS_EC_ENODEV;
-  if (max_devices > 0 && max_devices < ndev) ndev = max_devices;
-  if (count == 0) return VDS_EC_OK;
-  // Validate every object before any transfer, as restore16_host does per
-  // object (chunk.h:415-419 lengths; the trailer of the first chunk), so a
-  // bad object fails the call without partial output.
-  const bool cells = (flags & VDS_EC_F_CELLS) != 0;
-  std::vector<uint64_t> lens(count);
-  for (uint32_t o = 0; o < count; ++o) {
-    const uint64_t cs = chunk_sizes[o];
-    int rc = check_restore_args(k, nodes + (uint64_t)o * k, chunks + (uint64_t)o * k, cs);
-    if (rc) return rc;
-    const uint8_t *c0 = chunks[(uint64_t)o * k];
-    const uint16_t padding = (cells || cs < 2) ? 0 : (uint16_t)((c0[cs - 2] << 8) | c0[cs - 1]);
-    bool ok = true;
-    lens[o] = restored_len(2, k, cs, padding, flags, &ok);
-    if (!ok) return VDS_EC_ERESTORE;
-    if (lens[o] > out_sizes[o] || (lens[o] && !outs[o])) return VDS_EC_EINVAL;
-  }
-  std::atomic<int> status{VDS_EC_OK};
-  auto worker = [&](int dev) {
-    if (hipSetDevice(dev) != hipSuccess) {
-      status = VDS_EC_ENODEV;
-      return;
-    }
-    // The encode batch's ring: while one slot's object is on the GPU, the
-    // other slot's pinned staging is filled with the next object's chunks or
-    // drained into the caller's buffer.
-    BatchRing *ring = batch_ring(dev);
-    if (!ring) {
-      status = VDS_EC_ENODEV;
-      return;
-    }
-    std::lock_guard<std::mutex> hold(ring->mu);
-    auto drain = [&](BatchSlot &s) -> int {
-      if (s.obj < 0) return VDS_EC_OK;
-      hipError_t e = hipStreamSynchronize(s.stream);
-      if (e != hipSuccess) return hip_status(e);
-      if (lens[s.obj]) parallel_copy({{outs[s.obj], s.h_out}}, lens[s.obj]);
-      s.obj = -1;
-      return VDS_EC_OK;
-    };
-    int si = 0;
-    for (int64_t o = dev; o < (int64_t)count && status.load() == VDS_EC_OK; o += ndev, si ^= 1) {
-      BatchSlot &s = ring->slot[si];
-      int rc = drain(s);
-      if (rc) { status = rc; break; }
-      const uint64_t cs = chunk_sizes[o];
-      const uint16_t *nd = nodes + (uint64_t)o * k;
-      std::vector<uint16_t> m((size_t)k * k);
-      rc = inverse16(k, nd, m.data());
-      if (rc) { status = rc; break; }
-      rc = s.reserve(cs * k ? cs * k : 1, lens[o] ? lens[o] : 1);
-      if (rc) { status = rc; break; }
-      std::vector<std::pair<uint8_t *, const uint8_t *>> parts(k);
-      for (uint32_t j = 0; j < k; ++j) parts[j] = {s.h_in + (uint64_t)j * cs, chunks[(uint64_t)o * k + j]};
-      if (cs) parallel_copy(parts, cs);
-      hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, cs * k, hipMemcpyHostToDevice, s.stream);
-      if (e != hipSuccess) { status = hip_status(e); break; }
-      std::vector<const uint8_t *> dchunks(k);
-      for (uint32_t j = 0; j < k; ++j) dchunks[j] = s.d_in + (uint64_t)j * cs;
-      rc = restore_device(2, k, nd, m.data(), dchunks.data(), cs, 0, lens[o], 1, s.d_out, 0, flags, s.stream);
-      if (rc) { status = rc; break; }
-      if (lens[o]) {
-        e = hipMemcpyAsync(s.h_out, s.d_out, lens[o], hipMemcpyDeviceToHost, s.stream);
-        if (e != hipSuccess) { status = hip_status(e); break; }
-      }
-      s.obj = o;
-    }
-    for (auto &s : ring->slot) {
-      int rc = drain(s);
-      if (rc && status.load() == VDS_EC_OK) status = rc;
-      s.obj = -1;
-    }
-  };
-  std::vector<std::thread> threads;
-  for (int d = 0; d < ndev; ++d) threads.emplace_back(worker, d);
-  for (auto &t : threads) t.join();
-  if (status.load() == VDS_EC_OK)
-    for (uint32_t o = 0; o < count; ++o) out_sizes[o] = lens[o];
-  return status.load();
+  return restore_host_batch(k, nodes, chunks, chunk_sizes, count, outs, out_sizes, flags, max_devices);
 }
 
 int vds_ec_sha256_device(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count, uint8_t *digests,

@@ -231,8 +231,16 @@ def live_shape(torch, chunk, dev, stream, objects, steps, loss=0.02, seed=1):
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / steps, e0.elapsed_time(e1) / steps * 1e-3
 
+    # save_temp names every replica by its SHA-256 (dht_network_client.cpp:77-79):
+    # one launch over all n x objects replicas (n * objects messages of L bytes)
+    digests = torch.empty(n * objects * 32, dtype=torch.uint8, device=dev)
+
+    def sha():
+        chunk.sha256_device(reps, L, L, n * objects, digests, stream)
+
     with torch.cuda.stream(stream):
         enc_wall, enc_gpu = timed(enc)
+        sha_wall, sha_gpu = timed(sha)
         rest_wall, rest_gpu = timed(restore)
         regen_wall, regen_gpu = timed(regen) if len(rg) else (None, None)
     torch.cuda.synchronize(dev)
@@ -245,12 +253,19 @@ def live_shape(torch, chunk, dev, stream, objects, steps, loss=0.02, seed=1):
     res = {"shape": f"k={k}, n={n}, {objects} x 64 KiB objects; replica loss p={loss}; "
                     f"{len(objs)} restorable, {len(rg)} regenerated",
            "encode_GiBps": gib(objects * size, enc_gpu),
+           "sha256_replicas_GiBps": gib(n * objects * L, sha_gpu),
+           "sha256_object_GiBps": gib(objects * size, sha_gpu),
            "repair_GiBps": gib(len(objs) * size, rest_gpu),
            "repair_host_GiBps": gib(len(objs) * size, rest_wall),
            "regenerate_GiBps": gib(len(rg) * size, regen_gpu),
            "regenerate_host_GiBps": gib(len(rg) * size, regen_wall),
            "distinct_survivor_sets": int(len({tuple(r) for r in nodes.tolist()}))}
-    del inp, reps, out, rg_out
+    # spot-check the digests against hashlib
+    import hashlib
+    hb = reps.view(-1)[: 4 * L].cpu().numpy().tobytes()
+    dg = digests[: 4 * 32].cpu().numpy().tobytes()
+    assert all(hashlib.sha256(hb[i * L:(i + 1) * L]).digest() == dg[32 * i:32 * (i + 1)] for i in range(4)), "sha"
+    del inp, reps, out, rg_out, digests
     return res
 
 

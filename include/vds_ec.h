@@ -188,6 +188,31 @@ int vds_ec_restore16_host_batch(uint16_t k, const uint16_t *nodes, const uint8_t
                                 const uint64_t *chunk_sizes, uint32_t count, uint8_t *const *outs, uint64_t *out_sizes,
                                 unsigned flags, int max_devices);
 
+/* ---------------------------------------------------- stripe-range split
+ * One object split by stripe range [t0, t1), e.g. over GPUs.
+ * Cell t of every replica depends on stripe t alone, so the ranges are
+ * independent.  encode: in = the whole object (device, size bytes); writes
+ * replica bytes [2 t0, 2 t1) of outs[i] (whole replica buffers), and the
+ * trailer with the range that ends at T = ceil(size / 2k).  t0 < t1 <= T
+ * (T == 0: the range [0, 0), trailer only).  restore: chunks = the whole
+ * survivor buffers, padding = their trailer value; writes object bytes
+ * [2k t0, min(2k t1, E)) of out for t1 <= ceil(E / 2k) (E =
+ * vds_ec_restored_size).  Byte API only (no VDS_EC_F_CELLS).                */
+int vds_ec_encode16_range_device(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *in, uint64_t size,
+                                 uint64_t t0, uint64_t t1, uint8_t *const *outs, unsigned flags, void *stream);
+int vds_ec_restore16_range_device(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
+                                  uint16_t padding, uint64_t t0, uint64_t t1, uint8_t *out, unsigned flags,
+                                  void *stream);
+/* One host object over several GPUs: its stripes in `parts` ranges of whole
+ * 2048-stripe tiles (0 = one per device), range r on device r % devices, each
+ * with its own PCIe link.  Same arguments and results as
+ * vds_ec_encode16_host / vds_ec_restore16_host (out_size: capacity in,
+ * restored length out).                                                     */
+int vds_ec_encode16_host_split(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data, uint64_t size,
+                               uint8_t *const *outs, unsigned flags, int max_devices, uint32_t parts);
+int vds_ec_restore16_host_split(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
+                                uint8_t *out, uint64_t *out_size, unsigned flags, int max_devices, uint32_t parts);
+
 /* ---------------------------------------------------------- replica names
  * The reference names each replica by SHA-256 of its bytes (save_temp /
  * save_data: dht_network_client.cpp:79, :593 -> hash::signature(sha256),

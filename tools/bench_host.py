@@ -32,6 +32,7 @@ p.add_argument("--k", type=int, default=16)
 p.add_argument("--m", type=int, default=4)
 p.add_argument("--reps", type=int, default=2)
 p.add_argument("--live", type=int, default=0)
+p.add_argument("--split-mib", type=int, default=0, help="one object of this size over every GPU by stripe ranges")
 a = p.parse_args()
 k, n, size = a.k, a.k + a.m, a.object_mib << 20
 rng = np.random.default_rng(1)
@@ -124,9 +125,25 @@ def live(count, reps):
             "pcie_bytes_per_object_encode": size + n * L, "pcie_bytes_per_object_repair": k * L + size}
 
 
+def split(mib, reps):
+    size = mib << 20
+    obj = rng.integers(0, 256, size, dtype=np.uint8)
+    chunk.encode_host_split(k, ids, obj[: 1 << 20])  # warm-up
+    b = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = chunk.encode_host_split(k, ids, obj)
+        dt = time.perf_counter() - t0
+        b = dt if b is None else min(b, dt)
+    import torch
+    return {"object_bytes": size, "devices": torch.cuda.device_count(), "encode_GiBps": round(size / b / 2**30, 3),
+            "check": bool(np.array_equal(out[0][:1024], chunk.encode_host(k, [0], obj[:2 * k * 512])[0][:1024]))}
+
+
 print(json.dumps({"metric": "host-resident (PCIe-inclusive) encode / repair GiB/s", "objects": a.objects,
                   "object_bytes": size, "k": k, "n": n, "erased": erased,
                   "encode_GiBps": round(gib / best_enc, 3), "repair_GiBps": round(gib / best_rb, 3),
                   "repair_per_object_GiBps": round(gib / best_rep, 3),
                   "encode_s": round(best_enc, 4), "repair_s": round(best_rb, 4),
-                  "live": live(a.live, a.reps) if a.live else None}), flush=True)
+                  "live": live(a.live, a.reps) if a.live else None,
+                  "split": split(a.split_mib, a.reps) if a.split_mib else None}), flush=True)

@@ -81,6 +81,14 @@ SIGNATURES = {
                                               C.c_size_t, C.POINTER(C.c_size_t)]),
     "vds_ec_save_temp16_host": (C.c_int, [C.c_uint16, C.c_uint32, C.c_void_p, C.c_uint64, vpp, C.c_void_p,
                                           C.c_void_p, C.POINTER(C.c_uint32)]),
+    "vds_ec_encode16_range_device": (C.c_int, [C.c_uint16, u16p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64,
+                                               C.c_uint64, vpp, C.c_uint, C.c_void_p]),
+    "vds_ec_restore16_range_device": (C.c_int, [C.c_uint16, u16p, vpp, C.c_uint64, C.c_uint16, C.c_uint64,
+                                                C.c_uint64, C.c_void_p, C.c_uint, C.c_void_p]),
+    "vds_ec_encode16_host_split": (C.c_int, [C.c_uint16, u16p, C.c_uint32, C.c_void_p, C.c_uint64, vpp, C.c_uint,
+                                             C.c_int, C.c_uint32]),
+    "vds_ec_restore16_host_split": (C.c_int, [C.c_uint16, u16p, vpp, C.c_uint64, C.c_void_p, u64p, C.c_uint, C.c_int,
+                                              C.c_uint32]),
 }
 
 _lib = None

@@ -30,7 +30,8 @@ __all__ = [
     "encode_device", "restore_device", "fill_splitmix_device", "encode_host_batch", "restore_host_batch",
     "regenerate_host",
     "regenerate_device", "sha256_device", "encode_hash_host", "replica_storage_paths",
-    "VdsEcError", "multipliers", "inverse",
+    "VdsEcError", "multipliers", "inverse", "encode_range_device", "restore_range_device", "encode_host_split",
+    "restore_host_split",
 ]
 
 
@@ -249,6 +250,57 @@ def restore_device(k: int, nodes: Sequence[int], chunks: Sequence[int], chunk_si
     out_ptr = out.data_ptr() if hasattr(out, "data_ptr") else int(out)
     check(_lib.lib().vds_ec_restore16_device(k, _idp(ids, 2), ptrs, chunk_size, chunk_stride, padding, count,
                                              out_ptr, out_stride, 0, _stream_ptr(stream)), "restore16_device")
+
+
+def encode_range_device(k: int, replicas: Sequence[int], inp, size: int, t0: int, t1: int, outs: Sequence[int],
+                        write_padding: bool = True, stream=None) -> None:
+    """vds_ec_encode16_range_device: stripes [t0, t1) of one device object
+    into replica bytes [2 t0, 2 t1) of the whole replica buffers `outs`
+    (SURVEY.md 8(e) stripe-range split)."""
+    ids = _ids(replicas, 2)
+    ptrs = (C.c_void_p * max(1, ids.size))(*[int(o) for o in outs])
+    in_ptr = inp.data_ptr() if hasattr(inp, "data_ptr") else int(inp)
+    check(_lib.lib().vds_ec_encode16_range_device(k, _idp(ids, 2), ids.size, in_ptr, size, t0, t1, ptrs,
+                                                  0 if write_padding else F_NO_TRAILER, _stream_ptr(stream)),
+          "encode16_range_device")
+
+
+def restore_range_device(k: int, nodes: Sequence[int], chunks: Sequence[int], chunk_size: int, padding: int,
+                         t0: int, t1: int, out, stream=None) -> None:
+    """vds_ec_restore16_range_device: object bytes [2k t0, min(2k t1, E)) of
+    `out` from stripes [t0, t1) of the whole survivor buffers."""
+    ids = _ids(nodes, 2)
+    ptrs = (C.c_void_p * ids.size)(*[int(c) for c in chunks])
+    out_ptr = out.data_ptr() if hasattr(out, "data_ptr") else int(out)
+    check(_lib.lib().vds_ec_restore16_range_device(k, _idp(ids, 2), ptrs, chunk_size, padding, t0, t1, out_ptr, 0,
+                                                   _stream_ptr(stream)), "restore16_range_device")
+
+
+def encode_host_split(k: int, replicas: Sequence[int], data, parts: int = 0, max_devices: int = 0) -> list:
+    """One host object over the GPUs by stripe ranges (vds_ec_encode16_host_split);
+    returns the n replicas."""
+    ids = _ids(replicas, 2)
+    buf = _u8(data)
+    L = replica_size(k, buf.size)
+    outs = [np.empty(max(L, 1), dtype=np.uint8) for _ in range(ids.size)]
+    ptrs = (C.c_void_p * max(1, ids.size))(*[o.ctypes.data for o in outs])
+    check(_lib.lib().vds_ec_encode16_host_split(k, _idp(ids, 2), ids.size, buf.ctypes.data, buf.size, ptrs, 0,
+                                                max_devices, parts), "encode16_host_split")
+    return [o[:L] for o in outs]
+
+
+def restore_host_split(k: int, nodes: Sequence[int], chunks: Sequence, parts: int = 0, max_devices: int = 0):
+    """One object restored over the GPUs by stripe ranges from k host
+    replicas (vds_ec_restore16_host_split); returns the restored bytes."""
+    ids = _ids(nodes, 2)
+    bufs = [_u8(c) for c in chunks]
+    cs = bufs[0].size
+    out = np.empty(max(cs * k, 1), dtype=np.uint8)
+    n_out = C.c_uint64(out.size)
+    ptrs = (C.c_void_p * ids.size)(*[b.ctypes.data for b in bufs])
+    check(_lib.lib().vds_ec_restore16_host_split(k, _idp(ids, 2), ptrs, cs, out.ctypes.data, C.byref(n_out), 0,
+                                                 max_devices, parts), "restore16_host_split")
+    return out[: n_out.value]
 
 
 def restore_batch_device(k: int, nodes: Sequence[Sequence[int]], chunks: Sequence[Sequence[int]],

@@ -103,23 +103,26 @@ __global__ __launch_bounds__(64) void k_sha256(const uint8_t *base, uint64_t len
     sha256_compress(h, w);
   }
 
-  // The rest (< 132 bytes) byte by byte, then 0x80, zeros and the 64-bit
-  // big-endian bit length in the last block.
-  const uint8_t *tail = m + 64 * nfast;
+  // The rest (< 132 bytes) the same way, from the aligned dwords that hold at
+  // least one message byte (never past the dword of the last byte), then
+  // bytes >= rem masked off, 0x80 after them, and the 64-bit big-endian bit
+  // length in the last block.
   const uint64_t rem = len - 64 * nfast;
   const uint32_t nb = (uint32_t)((rem + 9 + 63) / 64);
   const uint64_t bits = len * 8;
+  const uint64_t lim = len + sh;  // aligned byte offsets < lim hold message bytes
   for (uint32_t blk = 0; blk < nb; ++blk) {
+    const uint64_t q0 = 16 * (nfast + blk);
+    uint32_t raw[17];
+#pragma unroll
+    for (int i = 0; i <= 16; ++i) raw[i] = 4 * (q0 + i) < lim ? p[q0 + i] : 0u;
     uint32_t w[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const uint64_t pos = 64ull * blk + 4 * i + t;
-        const uint32_t byte = pos < rem ? tail[pos] : (pos == rem ? 0x80u : 0u);
-        v = (v << 8) | byte;
-      }
+      const int64_t c = (int64_t)rem - (int64_t)(64 * blk + 4 * i);  // message bytes left at this word
+      uint32_t v = __builtin_amdgcn_perm(raw[i + 1], raw[i], sel);
+      if (c < 4) v = c <= 0 ? 0u : v & ~(0xFFFFFFFFu >> (8 * c));
+      if (c >= 0 && c < 4) v |= 0x80u << (24 - 8 * c);
       w[i] = v;
     }
     if (blk + 1 == nb) {

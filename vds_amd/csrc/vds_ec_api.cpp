@@ -1510,6 +1510,142 @@ int restore_host_batch(uint32_t k, const uint16_t *nodes, const uint8_t *const *
   return rc;
 }
 
+// ------------------------------------------------ stripe-range split
+// One object split by stripe range [t0, t1): cell t of every
+// replica depends on stripe t only, so a range is encoded as an object of its
+// own -- the slice of input bytes [2k t0, 2k t1) (the object's last range: to
+// its end, zero-padded and with the trailer, whose value depends only on
+// size mod 2k) -- into replica bytes [2 t0, 2 t1).  Restore likewise writes
+// output bytes [2k t0, min(2k t1, E)) from the survivors' cells [t0, t1).
+int encode_range(uint32_t k, const uint16_t *replicas, uint32_t n, const uint8_t *in, uint64_t size, uint64_t t0,
+                 uint64_t t1, uint8_t *const *outs, unsigned flags, hipStream_t s) {
+  if (k == 0 || (flags & VDS_EC_F_CELLS) || (n && (!replicas || !outs))) return VDS_EC_EINVAL;
+  const uint64_t sb = 2ull * k, T = (size + sb - 1) / sb;
+  if (t0 > t1 || t1 > T || (t0 == t1 && T != 0)) return VDS_EC_EINVAL;
+  const bool last = t1 == T;
+  const uint64_t slice = last ? size - sb * t0 : sb * (t1 - t0);
+  std::vector<uint8_t *> o(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!outs[i]) return VDS_EC_EINVAL;
+    o[i] = outs[i] + 2 * t0;
+  }
+  return encode_device(2, k, replicas, n, in + sb * t0, slice, slice, 1, o.data(), 0,
+                       last ? flags : (flags | VDS_EC_F_NO_TRAILER), s);
+}
+
+// restored length and stripes of an object from its trailer padding
+int range_restore_len(uint32_t k, uint64_t chunk_size, uint16_t padding, unsigned flags, uint64_t *E, uint64_t *nst) {
+  if (flags & VDS_EC_F_CELLS) return VDS_EC_EINVAL;
+  bool ok = true;
+  *E = restored_len(2, k, chunk_size, padding, flags, &ok);
+  if (!ok) return VDS_EC_ERESTORE;
+  *nst = (*E + 2ull * k - 1) / (2ull * k);
+  return VDS_EC_OK;
+}
+
+int restore_range(uint32_t k, const uint16_t *nodes, const uint16_t *matrix, const uint8_t *const *chunks,
+                  uint64_t t0, uint64_t t1, uint64_t E, uint8_t *out, unsigned flags, hipStream_t s) {
+  const uint64_t sb = 2ull * k;
+  std::vector<const uint8_t *> c(k);
+  for (uint32_t j = 0; j < k; ++j) c[j] = chunks[j] + 2 * t0;
+  const uint64_t len = std::min(sb * t1, E) - sb * t0;
+  return restore_device(2, k, nodes, matrix, c.data(), 2 * (t1 - t0), 0, len, 1, out + sb * t0, 0, flags, s);
+}
+
+// Split [0, T) into `parts` ranges of whole 2048-stripe tiles (the last
+// takes the rest; fewer ranges when there are fewer tiles).
+std::vector<std::pair<uint64_t, uint64_t>> stripe_ranges(uint64_t T, uint32_t parts) {
+  std::vector<std::pair<uint64_t, uint64_t>> r;
+  const uint64_t tiles = (T + kTileStripes - 1) / kTileStripes;
+  const uint64_t p = std::max<uint64_t>(1, std::min<uint64_t>(parts, tiles));
+  uint64_t at = 0;
+  for (uint64_t i = 0; i < p; ++i) {
+    const uint64_t end = i + 1 == p ? T : std::min(T, (tiles * (i + 1) / p) * kTileStripes);
+    r.push_back({at, end});
+    at = end;
+  }
+  return r;
+}
+
+int encode_host_split(uint32_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data, uint64_t size,
+                      uint8_t *const *outs, unsigned flags, int max_devices, uint32_t parts) {
+  if (k == 0 || (flags & VDS_EC_F_CELLS) || (n && (!replicas || !outs)) || (size && !data)) return VDS_EC_EINVAL;
+  int ndev = 0;
+  int rc = batch_devices(max_devices, &ndev);
+  if (rc) return rc;
+  if (n == 0) return VDS_EC_OK;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!outs[i]) return VDS_EC_EINVAL;
+  const uint64_t sb = 2ull * k, T = (size + sb - 1) / sb;
+  const auto ranges = stripe_ranges(T, parts ? parts : (uint32_t)ndev);
+  std::vector<Group> groups;
+  for (uint32_t r = 0; r < ranges.size(); ++r) groups.push_back({r, 1});
+  const bool trailer = !(flags & VDS_EC_F_NO_TRAILER);
+  return run_host_batch(groups, ndev, [&](BatchSlot &s, const Group &g) -> int {
+    const auto [t0, t1] = ranges[g.o0];
+    const bool last = t1 == T;
+    const uint64_t in_b = last ? size - sb * t0 : sb * (t1 - t0);
+    const uint64_t Lr = 2 * (t1 - t0) + (last && trailer ? 2 : 0);  // replica bytes of the range
+    int rc = s.reserve(in_b, n * Lr);
+    if (rc) return rc;
+    parallel_copy({{s.h_in, data + sb * t0, in_b}});
+    hipError_t e = in_b ? hipMemcpyAsync(s.d_in, s.h_in, in_b, hipMemcpyHostToDevice, s.stream) : hipSuccess;
+    if (e != hipSuccess) return hip_status(e);
+    std::vector<uint8_t *> douts(n);
+    for (uint32_t i = 0; i < n; ++i) douts[i] = s.d_out + i * Lr;
+    rc = encode_device(2, k, replicas, n, s.d_in, in_b, in_b, 1, douts.data(), 0,
+                       last ? flags : (flags | VDS_EC_F_NO_TRAILER), s.stream);
+    if (rc) return rc;
+    e = hipMemcpyAsync(s.h_out, s.d_out, n * Lr, hipMemcpyDeviceToHost, s.stream);
+    if (e != hipSuccess) return hip_status(e);
+    s.out_parts.resize(n);
+    for (uint32_t i = 0; i < n; ++i) s.out_parts[i] = {outs[i] + 2 * t0, s.h_out + i * Lr, Lr};
+    return VDS_EC_OK;
+  });
+}
+
+int restore_host_split(uint32_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
+                       uint8_t *out, uint64_t *out_size, unsigned flags, int max_devices, uint32_t parts) {
+  int rc = check_restore_args(k, nodes, chunks, chunk_size);
+  if (rc) return rc;
+  if (!out_size || (flags & VDS_EC_F_CELLS)) return VDS_EC_EINVAL;
+  int ndev = 0;
+  if ((rc = batch_devices(max_devices, &ndev))) return rc;
+  const uint16_t padding = chunk_size < 2 ? 0 : (uint16_t)((chunks[0][chunk_size - 2] << 8) | chunks[0][chunk_size - 1]);
+  uint64_t E = 0, nst = 0;
+  if ((rc = range_restore_len(k, chunk_size, padding, flags, &E, &nst))) return rc;
+  if (E > *out_size || (E && !out)) return VDS_EC_EINVAL;
+  std::vector<uint16_t> m((size_t)k * k);
+  if ((rc = inverse16(k, nodes, m.data()))) return rc;
+  const uint64_t sb = 2ull * k;
+  const auto ranges = stripe_ranges(nst, parts ? parts : (uint32_t)ndev);
+  std::vector<Group> groups;
+  for (uint32_t r = 0; r < ranges.size() && nst; ++r) groups.push_back({r, 1});
+  rc = run_host_batch(groups, ndev, [&](BatchSlot &s, const Group &g) -> int {
+    const auto [t0, t1] = ranges[g.o0];
+    const uint64_t Lr = 2 * (t1 - t0), len = std::min(sb * t1, E) - sb * t0;
+    int rc = s.reserve(k * Lr, len);
+    if (rc) return rc;
+    std::vector<Copy> in(k);
+    std::vector<const uint8_t *> dchunks(k);
+    for (uint32_t j = 0; j < k; ++j) {
+      in[j] = {s.h_in + j * Lr, chunks[j] + 2 * t0, Lr};
+      dchunks[j] = s.d_in + j * Lr;
+    }
+    parallel_copy(in);
+    hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, k * Lr, hipMemcpyHostToDevice, s.stream);
+    if (e != hipSuccess) return hip_status(e);
+    rc = restore_device(2, k, nodes, m.data(), dchunks.data(), Lr, 0, len, 1, s.d_out, 0, flags, s.stream);
+    if (rc) return rc;
+    e = hipMemcpyAsync(s.h_out, s.d_out, len, hipMemcpyDeviceToHost, s.stream);
+    if (e != hipSuccess) return hip_status(e);
+    s.out_parts.assign(1, Copy{out + sb * t0, s.h_out, len});
+    return VDS_EC_OK;
+  });
+  if (rc == VDS_EC_OK) *out_size = E;
+  return rc;
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -1722,6 +1858,35 @@ int vds_ec_restore16_host_batch(uint16_t k, const uint16_t *nodes, const uint8_t
                                 const uint64_t *chunk_sizes, uint32_t count, uint8_t *const *outs, uint64_t *out_sizes,
                                 unsigned flags, int max_devices) {
   return restore_host_batch(k, nodes, chunks, chunk_sizes, count, outs, out_sizes, flags, max_devices);
+}
+
+int vds_ec_encode16_range_device(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *in, uint64_t size,
+                                 uint64_t t0, uint64_t t1, uint8_t *const *outs, unsigned flags, void *stream) {
+  return encode_range(k, replicas, n, in, size, t0, t1, outs, flags, as_stream(stream));
+}
+
+int vds_ec_restore16_range_device(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
+                                  uint16_t padding, uint64_t t0, uint64_t t1, uint8_t *out, unsigned flags,
+                                  void *stream) {
+  int rc = check_restore_args(k, nodes, chunks, chunk_size);
+  if (rc) return rc;
+  uint64_t E = 0, nst = 0;
+  if ((rc = range_restore_len(k, chunk_size, padding, flags, &E, &nst))) return rc;
+  if (t0 > t1 || t1 > nst || (E && !out)) return VDS_EC_EINVAL;
+  if (t0 == t1) return VDS_EC_OK;
+  std::vector<uint16_t> m((size_t)k * k);
+  if ((rc = inverse16(k, nodes, m.data()))) return rc;
+  return restore_range(k, nodes, m.data(), chunks, t0, t1, E, out, flags, as_stream(stream));
+}
+
+int vds_ec_encode16_host_split(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data, uint64_t size,
+                               uint8_t *const *outs, unsigned flags, int max_devices, uint32_t parts) {
+  return encode_host_split(k, replicas, n, data, size, outs, flags, max_devices, parts);
+}
+
+int vds_ec_restore16_host_split(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
+                                uint8_t *out, uint64_t *out_size, unsigned flags, int max_devices, uint32_t parts) {
+  return restore_host_split(k, nodes, chunks, chunk_size, out, out_size, flags, max_devices, parts);
 }
 
 int vds_ec_sha256_device(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count, uint8_t *digests,

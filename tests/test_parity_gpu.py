@@ -560,3 +560,32 @@ def test_large_k_parameters_are_stream_ordered(ec):
             assert np.array_equal(out[:size].cpu().numpy(), host), (k, nodes)
             for i, r in enumerate(tg):
                 assert np.array_equal(ro[i].cpu().numpy(), O.encode(k, r, host)), (k, nodes, r)
+
+
+@pytest.mark.parametrize("k,n", [(16, 20), (32, 64)])
+def test_host_batches_pack_groups(ec, k, n):
+    """The host batches pack runs of equal-size objects into groups of up to
+    64 MiB (several groups per run, the three-slot ring reused, size changes
+    between runs, empty objects); every replica equals the one-object host
+    encode (itself oracle-checked above; two objects re-checked here against
+    the oracle), and the batched restore from a survivor set per object gives
+    every object back."""
+    from vds_amd import chunk
+    rng = np.random.default_rng(90 + k)
+    sizes = [65536] * 400 + [3 << 20] * 3 + [0, 17] + [65536] * 7 + [2 * k * 2048 + 5] * 2
+    objs = [rng.integers(0, 256, s, dtype=np.uint8) for s in sizes]
+    ids = list(range(n))
+    reps = ec.encode_host_batch(k, ids, objs)
+    for i, d in enumerate(objs):
+        if i % 37 == 0 or i >= 400:
+            want = chunk.encode_host(k, ids, d)
+            assert all(np.array_equal(a, b) for a, b in zip(reps[i], want)), (i, d.size)
+    for i in (5, 401):
+        assert np.array_equal(reps[i][n - 1], O.encode(k, n - 1, objs[i]))
+    nodes = []
+    for _ in objs:  # restore_async: the first k replicas found per object
+        gone = set(rng.choice(n, n - k, replace=False).tolist()) if rng.random() < 0.7 else set()
+        nodes.append([r for r in range(n) if r not in gone][:k])
+    got = ec.restore_host_batch(k, nodes, [[reps[o][r] for r in nd] for o, nd in enumerate(nodes)])
+    for g, d in zip(got, objs):
+        assert np.array_equal(g, d), d.size

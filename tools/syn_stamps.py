@@ -1,7 +1,7 @@
 """Per-phase cycle breakdown of k_restore_syn from the VDS_DIAG_STAMPS build.
 
   python -c "from vds_amd import build as b; b.build(out='build/stamps.so', defines=('-DVDS_DIAG_STAMPS=1',))"
-  VDS_EC_LIB=build/stamps.so python tools/syn_stamps.py [--objects 128]
+  VDS_EC_LIB=build/stamps.so python tools/syn_stamps.py [--objects 128] [--k 32]
 
 Each wave sums s_memtime deltas per phase over its tiles; this prints the
 mean per tile of every phase, per wave and overall (barrier phases are the
@@ -21,19 +21,21 @@ from vds_amd import _lib, chunk  # noqa: E402
 PHASES = ["stage1 transposes+puts", "B1", "syndrome+load issue", "recovery walk", "B2", "ds_xor scatter", "B3",
           "stage A", "B(stage A)", "stage B programs", "B(Q read)", "P0/P1 puts", "B(P put)", "stage C",
           "B(stage C read)", "staging transposes+writes", "B(staging)", "copy-out stores", "B(tile end)", "-"]
-WV, NPH = 4, 20
+NPH = 20
 
 p = argparse.ArgumentParser()
 p.add_argument("--objects", type=int, default=128)
+p.add_argument("--k", type=int, default=16, choices=(16, 32))
 a = p.parse_args()
-k, n, size = 16, 20, 64 << 20
+k, n, size = a.k, a.k + a.k // 4, 64 << 20
+WV = 4 if k == 16 else 8
 L = chunk.replica_size(k, size)
 inp = torch.empty(a.objects * size, dtype=torch.uint8, device="cuda")
 reps = torch.empty((n, a.objects * L), dtype=torch.uint8, device="cuda")
 out = torch.empty(a.objects * size, dtype=torch.uint8, device="cuda")
 for i in range(a.objects):
     chunk.fill_splitmix_device(inp[i * size:], size, 0x7664730000000000 + i)
-nodes = [r for r in range(n) if r not in (0, 5, 10, 15)]
+nodes = [r for r in range(n) if r % 5 != 0 or r >= 5 * (n - k)][:k]
 chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, [reps[i].data_ptr() for i in range(n)], L)
 cp = [reps[r].data_ptr() for r in nodes]
 for _ in range(2):
@@ -43,7 +45,7 @@ lib = _lib.lib()
 buf = np.zeros(4096 * 4 * NPH, dtype=np.uint64)
 rc = lib.vds_ec_diag_stamps(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), C.c_size_t(buf.size))
 assert rc == 0, rc
-grid = 512
+grid = 512 if k == 16 else 256
 total_tiles = a.objects * size // (2048 * 2 * k)
 per_block = total_tiles / grid
 st = buf[: grid * WV * NPH].reshape(grid, WV, NPH).astype(np.float64) / per_block

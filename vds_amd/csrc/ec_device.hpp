@@ -53,6 +53,18 @@ template <class T>
 __device__ __forceinline__ T s_ld(const T *p) {
   return *(const __attribute__((address_space(4))) T *)p;
 }
+// Byte i of a wave-uniform launch table (e.g. a kernel argument's uint8_t
+// array at a runtime index; `arr` 4-byte aligned).  gfx950 has no sub-dword
+// scalar load: a plain arr[i] becomes a *vector* global_load_ubyte, whose
+// s_waitcnt vmcnt(0) then waits for every load and store the wave has in
+// flight -- at the top of a tile loop, the previous tile's stores and the
+// prefetched next tile.  Load the aligned dword with s_load and extract the
+// byte instead.  (No pointer-to-integer casts: on a kernel argument they
+// force a private copy of the whole argument struct.)
+__device__ __forceinline__ uint32_t s_ld_u8(const uint8_t *arr, int i) {
+  const uint32_t w = s_ld(reinterpret_cast<const uint32_t *>(arr) + (i >> 2));
+  return (w >> (8 * (i & 3))) & 0xFFu;
+}
 
 // The 16 planes of one cell from LDS as four ds_read_b128.  A volatile
 // 128-bit load through an LDS (address_space(3)) pointer keeps the compiler

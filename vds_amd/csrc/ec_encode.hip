@@ -76,6 +76,21 @@ struct EncodeShape {
   __device__ __forceinline__ static constexpr int cell_off(int c) { return 16 * c + kGroupPad * (c >> 2); }
 };
 
+// Replica r's output pointer, read from the kernel arguments where it is used.
+// Left to itself the compiler hoists all N pointers out of the tile loop; at
+// N = 40 or 64 they do not fit the SGPRs, spill to scratch, and every scratch
+// reload's s_waitcnt vmcnt(0) then waits for all the stores in flight (28-41
+// such drains per tile).  The opaque zero keeps the s_load at its use, and
+// the pointer comes from the kernarg segment itself (the kernel's only
+// explicit argument, at offset 0): indexing the by-value parameter at a
+// runtime index makes the compiler copy the whole struct to scratch.
+__device__ __forceinline__ uint8_t *rep_ptr(const FastEncodeArgs &, int r) {
+  int z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  const auto *k = (const __attribute__((address_space(4))) FastEncodeArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+  return k->outs[r + z];
+}
+
 // Transpose one replica's planes back to big-endian cells and store them.
 // After the transpose, word q of lane l holds the cells of stripes l + 64 q
 // (low half) and l + 1024 + 64 q (high half); each half goes out as a 2-byte
@@ -191,7 +206,7 @@ __device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const Fa
 #pragma unroll
     for (int s = S0; s < S0 + PR && s < RPW; ++s)
       if (S::kPlan.rep[W][s] == 0)
-        store_rep<S::kMap, ST>(lds_planes(set_planes + S::cell_off(0)), a.outs[0], a, tp, lane, bm);
+        store_rep<S::kMap, ST>(lds_planes(set_planes + S::cell_off(0)), rep_ptr(a, 0), a, tp, lane, bm);
     return;
   }
   Plane16 A[PR], B[PR];
@@ -213,8 +228,8 @@ __device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const Fa
 #pragma unroll
   for (int s = 0; s < PR; ++s) {
     const int r = S0 + s < RPW ? S::kPlan.rep[W][S0 + s] : -1;
-    if (r == 0) store_rep<S::kMap, ST>(xa, a.outs[0], a, tp, lane, bm);
-    if (r > 0) store_rep<S::kMap, ST>(A[s], a.outs[r], a, tp, lane, bm);
+    if (r == 0) store_rep<S::kMap, ST>(xa, rep_ptr(a, 0), a, tp, lane, bm);
+    if (r > 0) store_rep<S::kMap, ST>(A[s], rep_ptr(a, r), a, tp, lane, bm);
   }
   __builtin_amdgcn_s_setprio(0);
 }
@@ -257,7 +272,8 @@ __device__ __forceinline__ void encode_zero_dispatch(int wave, const FastEncodeA
     if (wave == W) {
 #pragma unroll
       for (int s = 0; s < RPW; ++s)
-        if (S::kPlan.rep[W][s] >= 0) store_rep<S::kMap, ST>(plane_zero(), a.outs[S::kPlan.rep[W][s]], a, tp, lane, bm);
+        if (S::kPlan.rep[W][s] >= 0)
+          store_rep<S::kMap, ST>(plane_zero(), rep_ptr(a, S::kPlan.rep[W][s]), a, tp, lane, bm);
     } else {
       encode_zero_dispatch<K, N, RPW, WV, ST, W + 1>(wave, a, tp, lane, bm);
     }

@@ -372,7 +372,7 @@ void k_restore_syn(SynRestoreArgs a) {
     const uint32_t o = BATCH ? 0u : obj_of(tile);  // (non-batch)
     const uint64_t stripe0 = BATCH ? 0u : stripe0_of(tile);
     const SynBatchPlan *pl = BATCH ? &a.plans[s_ld(&a.tiles[tile].plan)] : nullptr;
-    auto erased_of = [&](int m) -> int { return BATCH ? s_ld(&pl->erased[m]) : a.erased[m]; };
+    auto erased_of = [&](int m) -> int { return (int)s_ld_u8(BATCH ? pl->erased : a.erased, m); };
     const int my_erased = wave < S::kM ? erased_of(wave) : 0;
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
     {
@@ -392,7 +392,7 @@ void k_restore_syn(SynRestoreArgs a) {
         uint32_t Pl[16];
 #pragma unroll
         for (int b = 0; b < 16; ++b) Pl[b] = W[b ^ 8];
-        syn_put_point(L, BATCH ? s_ld(&pl->point[wave * S::kLoadPer + s]) : a.point[wave * S::kLoadPer + s], Pl);
+        syn_put_point(L, (int)s_ld_u8(BATCH ? pl->point : a.point, wave * S::kLoadPer + s), Pl);
       }
     }
     st.mark(0);

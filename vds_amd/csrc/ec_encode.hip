@@ -49,6 +49,46 @@ constexpr ReplicaPlan<N, WAVES, RPW> plan_replicas() {
   return p;
 }
 
+// ---- one-level additive split of the stripe polynomial.  The Taylor
+// expansion at z^2 + z (XORs only) gives P(z) = P0(y) + z P1(y), y = z^2 + z,
+// deg P0, P1 < K/2; y is the same for z = r and r + 1 (r even: char 2), so
+// P(r) = P0(y) + r P1(y) and P(r + 1) = P(r) + P1(y).  A pair of replicas
+// costs two K/2-step Horners with the constant y, against two K-step Horners
+// with r and r + 1: 64-70% of the row-form XORs for n = 20, 40, 64 (the first
+// level of the additive FFT of tools/xorgen/gen_encode_gm.py, without its
+// register-hungry deeper levels).
+constexpr uint32_t pair_y(int r) { return gf16_mul((uint32_t)r, (uint32_t)r) ^ (uint32_t)r; }
+constexpr int pair_cost(int r) { return 2 * horner_cost((int)pair_y(r)) + 1; }
+
+template <int WAVES, int PPW>
+struct PairPlan {
+  int r[WAVES][PPW];  // even r of the pair (r, r + 1); -1: empty
+};
+
+template <int N, int WAVES, int PPW>
+constexpr PairPlan<WAVES, PPW> plan_pairs() {
+  PairPlan<WAVES, PPW> p{};
+  int load[WAVES] = {};
+  int cnt[WAVES] = {};
+  bool used[N / 2 + 1] = {};
+  int cost[N / 2 + 1] = {};
+  for (int q = 0; q < N / 2; ++q) cost[q] = pair_cost(2 * q);  // (once each: constexpr step limit)
+  for (int w = 0; w < WAVES; ++w)
+    for (int s = 0; s < PPW; ++s) p.r[w][s] = -1;
+  for (int it = 0; it < N / 2; ++it) {
+    int best = -1;
+    for (int q = 0; q < N / 2; ++q)
+      if (!used[q] && (best < 0 || cost[q] > cost[best])) best = q;
+    used[best] = true;
+    int bw = -1;
+    for (int w = 0; w < WAVES; ++w)
+      if (cnt[w] < PPW && (bw < 0 || load[w] < load[bw])) bw = w;
+    p.r[bw][cnt[bw]++] = 2 * best;
+    load[bw] += cost[best];
+  }
+  return p;
+}
+
 template <int K, int N, int RPW, int WV>
 struct EncodeShape {
   // Loads: every lane takes two dwords (4 cells) of each of its set's 32
@@ -71,6 +111,8 @@ struct EncodeShape {
   static constexpr int kWavesPerSimd = 2;  // 256 VGPRs: accumulators ping-pong + the prefetched tile
   static constexpr int kMap = kLanesPerSet >= 2 ? 3 : 0;  // slot map (store_replica_groups); k = 4: 0
   static constexpr ReplicaPlan<N, kWaves, RPW> kPlan = plan_replicas<N, kWaves, RPW>();
+  static constexpr int kPPW = (N / 2 + kWaves - 1) / kWaves;  // replica pairs per wave (split mode)
+  static constexpr PairPlan<kWaves, kPPW> kPairs = plan_pairs<N, kWaves, kPPW>();
   static_assert(K % 4 == 0 && WV == K / 4, "fast encode: k % 4 == 0 and k/4 waves");
   static_assert(RPW * WV >= N, "every replica needs a wave");
   __device__ __forceinline__ static constexpr int cell_off(int c) { return 16 * c + kGroupPad * (c >> 2); }
@@ -282,6 +324,141 @@ __device__ __forceinline__ void encode_zero_dispatch(int wave, const FastEncodeA
   }
 }
 
+// ---- split mode
+
+// In-place Taylor expansion at z^2 + z of c[OFF .. OFF + NN) (NN a power of
+// two): blocks C0..C3 of NN/4: C2 ^= C3, C1 ^= C2, then each half.  Cell 2i
+// ends as the coefficient i of P0, cell 2i + 1 as that of P1.
+template <int K, int OFF, int NN>
+__device__ __forceinline__ void taylor_inplace(u32x4 (&c)[K]) {
+  if constexpr (NN > 2) {
+    constexpr int t = NN / 4;
+#pragma unroll
+    for (int i = 0; i < t; ++i) c[OFF + 2 * t + i] ^= c[OFF + 3 * t + i];
+#pragma unroll
+    for (int i = 0; i < t; ++i) c[OFF + t + i] ^= c[OFF + 2 * t + i];
+    taylor_inplace<K, OFF, 2 * t>(c);
+    taylor_inplace<K, OFF + 2 * t, 2 * t>(c);
+  }
+}
+
+// The tile's sets in LDS -> their Taylor coefficients, in place; plane-
+// parallel (the XORs never mix planes): wave w < 4 takes planes 4w..4w+3 of
+// every cell (one ds_read_b128 / ds_write_b128 per cell, conflict-free as
+// the Horner reads).
+template <int K, int N, int RPW, int WV>
+__device__ __forceinline__ void taylor_lds(int wave, uint32_t *set_planes) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  if (wave < 4) {
+    u32x4 c[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) c[i] = *(lds_u32x4 *)(set_planes + S::cell_off(i) + 4 * wave);
+    taylor_inplace<K, 0, K>(c);
+#pragma unroll
+    for (int i = 0; i < K; ++i) *(lds_v4 *)(set_planes + S::cell_off(i) + 4 * wave) = c[i];
+  }
+}
+
+// dst[p] = src[p] * y_p + x for the pairs S0 .. S0+PP-1 of wave W
+template <int K, int N, int RPW, int WV, int W, int S0, int PP>
+__device__ __forceinline__ void pair_step(Plane16 (&dst)[PP], const Plane16 (&src)[PP], const Plane16 &x) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  [&]<size_t... I>(std::index_sequence<I...>) {
+    constexpr auto r = [](int i) { return S0 + i < S::kPPW ? S::kPairs.r[W][S0 + i] : -1; };
+    ((r(I) >= 0 ? (void)(dst[I] = plane_horner_rows<(r(I) >= 0 ? pair_y(r(I)) : 0u)>(src[I], x)) : (void)0), ...);
+  }(std::make_index_sequence<PP>{});
+}
+
+// Horner of P_H (H = 0: even cells, 1: odd cells) for the pairs S0.. of wave
+// W, two steps per iteration (A / B ping-pong, as encode_pass).
+template <int K, int N, int RPW, int WV, int W, int S0, int PP, int H>
+__device__ __forceinline__ void pair_half(const uint32_t *set_planes, Plane16 (&A)[PP]) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  constexpr int HK = K / 2;
+  auto X = [&](int c) { return lds_planes(set_planes + S::cell_off(2 * c + H)); };
+  Plane16 B[PP];
+  {
+    const Plane16 x = X(HK - 1);
+#pragma unroll
+    for (int p = 0; p < PP; ++p) A[p] = x;
+  }
+  Plane16 xa = X(HK - 2);
+#pragma clang loop unroll(disable)
+  for (int c = HK - 2; c >= 1; c -= 2) {
+    const Plane16 xb = X(c - 1);
+    pair_step<K, N, RPW, WV, W, S0, PP>(B, A, xa);
+    xa = X(c - 2);
+    pair_step<K, N, RPW, WV, W, S0, PP>(A, B, xb);
+  }
+  pair_step<K, N, RPW, WV, W, S0, PP>(A, A, xa);
+}
+
+template <int K, int N, bool ST>
+constexpr int pair_pass() {
+  return (K == 32 && N == 64) ? 2 : 3;
+}
+
+template <int K, int N, int RPW, int WV, int W, bool ST, int S0 = 0>
+__device__ __forceinline__ void encode_pair_group(const uint32_t *set_planes, const FastEncodeArgs &a, TilePos tp,
+                                                  int lane, const BitMasks &bm) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  constexpr int kP = pair_pass<K, N, ST>();
+  constexpr int PP = kP < S::kPPW ? kP : S::kPPW;
+  if constexpr (S0 < S::kPPW) {
+    Plane16 R0[PP], R1[PP];
+    pair_half<K, N, RPW, WV, W, S0, PP, 0>(set_planes, R0);
+    pair_half<K, N, RPW, WV, W, S0, PP, 1>(set_planes, R1);
+    __builtin_amdgcn_s_setprio(kEncStorePrio);
+    [&]<size_t... I>(std::index_sequence<I...>) {
+      constexpr auto r = [](int i) { return S0 + i < S::kPPW ? S::kPairs.r[W][S0 + i] : -1; };
+      auto one = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (r(i) >= 0) {
+          const Plane16 o0 = plane_xor(R0[i], plane_mulc<(uint32_t)(r(i) >= 0 ? r(i) : 0)>(R1[i]));
+          store_rep<S::kMap, ST>(o0, rep_ptr(a, r(i)), a, tp, lane, bm);
+          store_rep<S::kMap, ST>(plane_xor(o0, R1[i]), rep_ptr(a, r(i) + 1), a, tp, lane, bm);
+        }
+      };
+      (one(std::integral_constant<int, (int)I>{}), ...);
+    }(std::make_index_sequence<PP>{});
+    __builtin_amdgcn_s_setprio(0);
+    encode_pair_group<K, N, RPW, WV, W, ST, S0 + PP>(set_planes, a, tp, lane, bm);
+  }
+}
+
+template <int K, int N, int RPW, int WV, bool ST, int W>
+__device__ __forceinline__ void pair_dispatch(int wave, const uint32_t *set_planes, const FastEncodeArgs &a, TilePos tp,
+                                              int lane, const BitMasks &bm) {
+  if constexpr (W < WV) {
+    if (wave == W)
+      encode_pair_group<K, N, RPW, WV, W, ST>(set_planes, a, tp, lane, bm);
+    else
+      pair_dispatch<K, N, RPW, WV, ST, W + 1>(wave, set_planes, a, tp, lane, bm);
+  } else {
+    __builtin_unreachable();
+  }
+}
+
+template <int K, int N, int RPW, int WV, bool ST, int W>
+__device__ __forceinline__ void pair_zero_dispatch(int wave, const FastEncodeArgs &a, TilePos tp, int lane,
+                                                   const BitMasks &bm) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  if constexpr (W < WV) {
+    if (wave == W) {
+#pragma unroll
+      for (int s = 0; s < S::kPPW; ++s)
+        if (S::kPairs.r[W][s] >= 0) {
+          store_rep<S::kMap, ST>(plane_zero(), rep_ptr(a, S::kPairs.r[W][s]), a, tp, lane, bm);
+          store_rep<S::kMap, ST>(plane_zero(), rep_ptr(a, S::kPairs.r[W][s] + 1), a, tp, lane, bm);
+        }
+    } else {
+      pair_zero_dispatch<K, N, RPW, WV, ST, W + 1>(wave, a, tp, lane, bm);
+    }
+  } else {
+    __builtin_unreachable();
+  }
+}
+
 // k = 4: load dwords 2p, 2p+1 of the 32 stripes of set `set`; slot i <->
 // stripe stripe0 + s + 64 i (whole tiles of one object).  The data stays in
 // the loaded vector registers until the next iteration unpacks it, so no copy
@@ -337,8 +514,9 @@ __device__ __forceinline__ void encode_unpack16(const u32x4 (&V)[16], uint32_t (
 }
 
 // STREAM: tiles may straddle objects (groups_per_obj % 16 != 0, k >= 8); the
-// non-stream instantiation keeps one base address per tile.
-template <int K, int N, int RPW, int WV, bool STREAM>
+// non-stream instantiation keeps one base address per tile.  SPLIT: replica
+// pairs from the one-level split (Taylor coefficients in LDS).
+template <int K, int N, int RPW, int WV, bool STREAM, bool SPLIT>
 __global__ __launch_bounds__((EncodeShape<K, N, RPW, WV>::kThreads), (EncodeShape<K, N, RPW, WV>::kWavesPerSimd))
 void k_encode_bs(FastEncodeArgs a) {
   using S = EncodeShape<K, N, RPW, WV>;
@@ -349,7 +527,7 @@ void k_encode_bs(FastEncodeArgs a) {
   const int tset = wave * S::kSetsPerWave + lane / S::kLanesPerSet;
   const int tp = lane % S::kLanesPerSet;
   uint32_t *t_planes = lds + tset * S::kSetWords + S::cell_off(4 * tp);
-  const uint32_t *my_set = lds + lane * S::kSetWords;
+  uint32_t *my_set = lds + lane * S::kSetWords;
   const BitMasks bm = bit_masks();
 
   constexpr bool kLoad16 = S::kMap != 0;
@@ -378,7 +556,10 @@ void k_encode_bs(FastEncodeArgs a) {
     // Issuing the same stores here (zeros into this wave's replica cells of
     // its first tile, which that tile overwrites, in order, from the same
     // wave) makes both states alike.
-    encode_zero_dispatch<K, N, RPW, WV, STREAM, 0>(wave, a, tile_pos(a, tile), lane, bm);
+    if constexpr (SPLIT)
+      pair_zero_dispatch<K, N, RPW, WV, STREAM, 0>(wave, a, tile_pos(a, tile), lane, bm);
+    else
+      encode_zero_dispatch<K, N, RPW, WV, STREAM, 0>(wave, a, tile_pos(a, tile), lane, bm);
   }
   for (; tile < t_end; tile += t_step) {
     // ---- transpose to planes and publish in LDS: cell 4p+2g+h, bit b = R[g][16h + (b^8)]
@@ -409,15 +590,21 @@ void k_encode_bs(FastEncodeArgs a) {
     const uint32_t next = tile + t_step;
     if (next < t_end) load(next);
     // ---- evaluate this wave's replicas and store
-    encode_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
+    if constexpr (SPLIT) {
+      taylor_lds<K, N, RPW, WV>(wave, my_set);
+      __syncthreads();
+      pair_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
+    } else {
+      encode_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
+    }
     __syncthreads();
   }
 }
 
-template <int K, int N, int RPW, int WV, bool STREAM>
+template <int K, int N, int RPW, int WV, bool STREAM, bool SPLIT>
 static hipError_t launch_encode_bs_st(const FastEncodeArgs &a, hipStream_t s) {
   using S = EncodeShape<K, N, RPW, WV>;
-  hipError_t e = ensure_lds_attr(&k_encode_bs<K, N, RPW, WV, STREAM>, S::kLdsBytes);
+  hipError_t e = ensure_lds_attr(&k_encode_bs<K, N, RPW, WV, STREAM, SPLIT>, S::kLdsBytes);
   if (e != hipSuccess) return e;
   const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
   int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
@@ -425,15 +612,32 @@ static hipError_t launch_encode_bs_st(const FastEncodeArgs &a, hipStream_t s) {
   if (over) grid = (int)over;
   if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_encode_bs<K, N, RPW, WV, STREAM>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  hipLaunchKernelGGL((k_encode_bs<K, N, RPW, WV, STREAM, SPLIT>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
   return hipGetLastError();
+}
+
+// VDS_EC_ENCODE_PATH=horner: plain Horner where split mode is compiled (A/B).
+static bool encode_path_horner() {
+  static const bool h = [] {
+    const char *v = std::getenv("VDS_EC_ENCODE_PATH");
+    return v && v[0] == 'h';
+  }();
+  return h;
+}
+
+template <int K, int N, int RPW, int WV, bool SPLIT>
+static hipError_t launch_encode_bs_sp(const FastEncodeArgs &a, hipStream_t s) {
+  if (a.groups_per_obj % 16 == 0) return launch_encode_bs_st<K, N, RPW, WV, false, SPLIT>(a, s);
+  if constexpr (K >= 8) return launch_encode_bs_st<K, N, RPW, WV, true, SPLIT>(a, s);
+  return hipErrorNotSupported;
 }
 
 template <int K, int N, int RPW, int WV>
 static hipError_t launch_encode_bs(const FastEncodeArgs &a, hipStream_t s) {
-  if (a.groups_per_obj % 16 == 0) return launch_encode_bs_st<K, N, RPW, WV, false>(a, s);
-  if constexpr (K >= 8) return launch_encode_bs_st<K, N, RPW, WV, true>(a, s);
-  return hipErrorNotSupported;
+  if constexpr (K >= 16) {
+    if (!encode_path_horner()) return launch_encode_bs_sp<K, N, RPW, WV, true>(a, s);
+  }
+  return launch_encode_bs_sp<K, N, RPW, WV, false>(a, s);
 }
 
 bool has_encode_fast(uint32_t k, uint32_t n) {

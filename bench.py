@@ -170,8 +170,8 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
     call over all objects (vds_ec_restore16_batch_device), and one lost
     replica of 0..39 per object is regenerated (sync_process's repair) with
     vds_ec_regenerate16_batch_device.  Host times include the per-object
-    planning and table staging of the batched calls; the timed calls follow
-    max(3, warmup) untimed ones (by then the process-wide erased-set plans
+    planning and table staging of the batched calls; max(steps, 10) timed
+    calls follow max(5, warmup) untimed ones (by then the process-wide erased-set plans
     are solved and the pinned staging slots allocated, as in a running node)."""
     import ctypes as C
     import numpy as np
@@ -221,18 +221,20 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
             rg_sizes.ctypes.data_as(_lib.u64p), 1, rg_targets.ctypes.data_as(_lib.u16p),
             rg_outs.ctypes.data_as(_lib.vpp), sp))
 
+    reps_timed = max(steps, 10)  # (beside the metric: enough calls for a stable rate)
+
     def timed(fn):
-        for _ in range(max(3, warmup)):  # steady state: staging slots allocated, erased-set plans solved
+        for _ in range(max(5, warmup)):  # steady state: staging slots allocated, erased-set plans solved
             fn()
         torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record(stream)
-        for _ in range(steps):
+        for _ in range(reps_timed):
             fn()
         e1.record(stream)
         torch.cuda.synchronize(dev)
-        return (time.perf_counter() - t0) / steps, e0.elapsed_time(e1) / steps * 1e-3
+        return (time.perf_counter() - t0) / reps_timed, e0.elapsed_time(e1) / reps_timed * 1e-3
 
     # save_temp names every replica by its SHA-256 (dht_network_client.cpp:77-79):
     # one launch over all n x objects replicas (n * objects messages of L bytes)

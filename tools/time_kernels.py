@@ -1,7 +1,7 @@
 """Time the encode and repair launches on a resident batch (no correctness
 check: used for A/B of diagnostic variant builds via VDS_EC_LIB).
 
-  python tools/time_kernels.py [--objects 128] [--iters 5]
+  python tools/time_kernels.py [--objects 128] [--iters 5] [--k 16|32] [--check]
 """
 import argparse
 import os
@@ -16,15 +16,18 @@ p = argparse.ArgumentParser()
 p.add_argument("--objects", type=int, default=128)
 p.add_argument("--iters", type=int, default=5)
 p.add_argument("--tag", default=os.path.basename(os.environ.get("VDS_EC_LIB", "default")))
+p.add_argument("--k", type=int, default=16, choices=(16, 32))
+p.add_argument("--check", action="store_true", help="compare the restored objects with the input")
 a = p.parse_args()
-k, n, size = 16, 20, 64 << 20
+k, size = a.k, 64 << 20
+n = k + k // 4
 L = chunk.replica_size(k, size)
 inp = torch.empty(a.objects * size, dtype=torch.uint8, device="cuda")
 reps = torch.empty((n, a.objects * L), dtype=torch.uint8, device="cuda")
 out = torch.empty(a.objects * size, dtype=torch.uint8, device="cuda")
 for i in range(a.objects):
     chunk.fill_splitmix_device(inp[i * size:], size, 0x7664730000000000 + i)
-nodes = [r for r in range(n) if r not in (0, 5, 10, 15)]
+nodes = [r for r in range(n) if r % 5 != 0 or r >= 5 * (n - k)]  # erase 0, 5, 10, ..
 rp = [reps[i].data_ptr() for i in range(n)]
 cp = [reps[r].data_ptr() for r in nodes]
 enc = lambda: chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, rp, L)  # noqa: E731
@@ -42,5 +45,8 @@ for name, f in (("encode", enc), ("repair", rep)):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     res[name] = (ms, a.objects * size / (ms * 1e-3) / 2**30)
-print(f"{a.tag}: encode {res['encode'][0]:.3f} ms ({res['encode'][1]:.1f} GiB/s)  "
-      f"repair {res['repair'][0]:.3f} ms ({res['repair'][1]:.1f} GiB/s)", flush=True)
+ok = ""
+if a.check:
+    ok = " check " + ("ok" if torch.equal(out, inp) else "MISMATCH")
+print(f"{a.tag} k={k}: encode {res['encode'][0]:.3f} ms ({res['encode'][1]:.1f} GiB/s)  "
+      f"repair {res['repair'][0]:.3f} ms ({res['repair'][1]:.1f} GiB/s){ok}", flush=True)

@@ -84,6 +84,31 @@ __device__ __forceinline__ Plane16 lds_planes(const uint32_t *p) {
   return x;
 }
 
+// Tile order of the persistent tile loops.  Workgroups are dealt round-robin
+// over the 8 XCDs (workgroup b on XCD b mod 8), so a grid stride of single
+// tiles puts adjacent tiles -- adjacent 4 KiB pieces of every replica stream
+// -- on different XCDs.  With VDS_XCD_TILES each XCD instead walks its own
+// contiguous eighth of the tiles, its workgroups side by side
+// (tools/ubench/hbm_write.hip, the encode's 20-stream store shape: 5.24 ->
+// 5.47-5.61 TB/s).  Any order is correct; this one is for speed only.
+#ifndef VDS_XCD_TILES
+#define VDS_XCD_TILES 1
+#endif
+struct TileRange {
+  uint32_t first, end, step;
+};
+__device__ __forceinline__ TileRange tile_range(uint32_t total) {
+#if VDS_XCD_TILES
+  const uint32_t g = gridDim.x;
+  if ((g & 7u) == 0 && total >= g) {  // (every XCD range then has >= g/8 tiles)
+    const uint32_t x = blockIdx.x & 7u;
+    const uint32_t lo = (uint32_t)((uint64_t)total * x / 8), hi = (uint32_t)((uint64_t)total * (x + 1) / 8);
+    return {lo + (blockIdx.x >> 3), hi, g >> 3};
+  }
+#endif
+  return {blockIdx.x, total, gridDim.x};
+}
+
 // ------------------------------------------------------------ host helpers
 
 // Study override of a fast kernel's grid (workgroups), read once per launcher:

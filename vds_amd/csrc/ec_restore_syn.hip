@@ -251,8 +251,8 @@ __device__ __forceinline__ void st16_guard(uint8_t *p, u32x4 v, int64_t valid) {
 //     and scatters its share of every recovered point into the erased slots;
 //  3. interpolates cells kCells*w.. from the fixed points 0..K-1 and stores
 //     them big-endian.
-// Tiles are strided over the grid (one contiguous range of tiles per
-// workgroup measured slower: repair 1572 -> 1460 GiB/s).
+// Tiles are strided over each XCD's workgroups (tile_range; one contiguous
+// range of tiles per workgroup measured slower: repair 1572 -> 1460 GiB/s).
 // BATCH: one launch over the tiles of many objects, each with its own
 // survivors, erasure plan, size and output (SynBatchTile / SynBatchObj /
 // SynBatchPlan, read with wave-uniform scalar loads).  Each half of a tile
@@ -328,8 +328,9 @@ void k_restore_syn(SynRestoreArgs a) {
   // Q, so the values consumed by this tile's stage 1 die there instead of
   // staying live (as loop-carried state) through the programs until the load
   // (k = 32 spilled 203 VGPRs that way: 1.6x / 1.4x the algorithmic traffic).
+  const TileRange tr = tile_range(a.total_tiles);
   auto prefetch = [&](uint32_t t) {
-    if (t < a.total_tiles) {
+    if (t < tr.end) {
       load(t);
     } else {
 #pragma unroll
@@ -347,8 +348,8 @@ void k_restore_syn(SynRestoreArgs a) {
   // (batch: the guarded loads and descriptor addresses would not fit beside
   // the programs either)
   constexpr bool kLateLoad = (K == 32 || BATCH) && !REGEN;
-  const uint32_t t_step = gridDim.x;
-  prefetch(blockIdx.x);
+  const uint32_t t_step = tr.step;
+  prefetch(tr.first);
   // vmcnt counts loads and stores together and retires them in issue order.
   // In the loop, the 16 copy-out stores of a tile are issued after the next
   // tile's survivor loads, so the loads can be waited for with vmcnt(16 + ..)
@@ -360,15 +361,15 @@ void k_restore_syn(SynRestoreArgs a) {
   // wave's copy-out chunk of its first tile, which that tile's copy-out
   // overwrites, in order, from the same wave) makes both states alike.
   if constexpr (!REGEN && !BATCH) {  // (batch: guarded stores; nothing to mirror)
-    if (blockIdx.x < a.total_tiles) {
-      const uint32_t t0 = blockIdx.x;
+    if (tr.first < tr.end) {
+      const uint32_t t0 = tr.first;
       uint8_t *g0 = a.out + (uint64_t)(t0 / a.tiles_per_obj) * a.out_stride +
                     (uint64_t)(t0 % a.tiles_per_obj) * kTileStripes * (2 * K) + 16384u * wave + 16u * lane;
 #pragma unroll
       for (int i = 0; i < 16; ++i) g_st<8>(g0 + 1024 * i, u32x4{0u, 0u, 0u, 0u});
     }
   }
-  for (uint32_t tile = blockIdx.x; tile < a.total_tiles; tile += t_step) {
+  for (uint32_t tile = tr.first; tile < tr.end; tile += t_step) {
     const uint32_t o = BATCH ? 0u : obj_of(tile);  // (non-batch)
     const uint64_t stripe0 = BATCH ? 0u : stripe0_of(tile);
     const SynBatchPlan *pl = BATCH ? &a.plans[s_ld(&a.tiles[tile].plan)] : nullptr;

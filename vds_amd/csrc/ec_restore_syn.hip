@@ -216,6 +216,47 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
   }
 }
 
+// One coefficient-bit pair of the recovery walk: acc ^= T, T1 or T ^ T1 as
+// the pair's two bits select (two = bit b | bit b+1 << 8), in one asm block
+// with its own branches.  As plain C++ the three arms computed into
+// different registers and every merge block copied the sixteen planes back
+// (8 v_mov_b64 per product and bit pair: as many moves as XORs); here the
+// planes are updated in place.  (The compares write SCC: declared clobbered,
+// or a live SCC of the surrounding code is lost.)
+#define VDS_RS_C(i) [c##i] "+v"(acc.p[i])
+#define VDS_RS_A(i) [a##i] "v"(t.p[i])
+#define VDS_RS_B(i) [b##i] "v"(t1.p[i])
+#define VDS_RS_LIST(M) M(0), M(1), M(2), M(3), M(4), M(5), M(6), M(7), M(8), M(9), M(10), M(11), M(12), M(13), M(14), M(15)
+#define VDS_RS_SEQ(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
+#define VDS_RS_XA(i) "v_xor_b32 %[c" #i "], %[c" #i "], %[a" #i "]\n"
+#define VDS_RS_XB(i) "v_xor_b32 %[c" #i "], %[c" #i "], %[b" #i "]\n"
+#define VDS_RS_X3(i) "v_bitop3_b32 %[c" #i "], %[c" #i "], %[a" #i "], %[b" #i "] bitop3:0x96\n"
+__device__ __forceinline__ void rec_pair(Plane16 &acc, const Plane16 &t, const Plane16 &t1, uint32_t two) {
+  asm volatile(
+      "s_cmp_eq_u32 %[two], 1\n"
+      "s_cbranch_scc0 1f\n" VDS_RS_SEQ(VDS_RS_XA)
+      "s_branch 3f\n"
+      "1:\n"
+      "s_cmpk_eq_u32 %[two], 0x100\n"
+      "s_cbranch_scc0 2f\n" VDS_RS_SEQ(VDS_RS_XB)
+      "s_branch 3f\n"
+      "2:\n"
+      "s_cmpk_eq_u32 %[two], 0x101\n"
+      "s_cbranch_scc0 3f\n" VDS_RS_SEQ(VDS_RS_X3)
+      "3:\n"
+      : VDS_RS_LIST(VDS_RS_C)
+      : VDS_RS_LIST(VDS_RS_A), VDS_RS_LIST(VDS_RS_B), [two] "s"(two)
+      : "scc");
+}
+#undef VDS_RS_C
+#undef VDS_RS_A
+#undef VDS_RS_B
+#undef VDS_RS_LIST
+#undef VDS_RS_SEQ
+#undef VDS_RS_XA
+#undef VDS_RS_XB
+#undef VDS_RS_X3
+
 // Batch mode: the last tile of an object may run past its bytes.  Loads
 // beyond `valid` bytes read zeros and stores beyond it write nothing (byte by
 // byte for the one 16-byte piece that straddles the end).
@@ -431,12 +472,7 @@ void k_restore_syn(SynRestoreArgs a) {
           for (int m = 0; m < kMC; ++m) {
             const uint32_t sel = BATCH ? s_ld(&pl->solve_sel[m0 + m][b >> 2]) : a.solve_sel[m0 + m][b >> 2];
             const uint32_t two = (sel >> (8 * (b & 3) + wave)) & 0x101u;
-            if (two == 1u)
-              ce[m] = plane_xor(ce[m], tt);
-            else if (two == 0x100u)
-              ce[m] = plane_xor(ce[m], t1);
-            else if (two == 0x101u)
-              ce[m] = plane_xor3(ce[m], tt, t1);
+            rec_pair(ce[m], tt, t1, two);
           }
           if (b < 14) tt = plane_mulx(t1);
         }

@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-live", action="store_true", help="skip the live-shape line (k=32, n=64, 64 KiB objects)")
     p.add_argument("--live-objects", type=int, default=16384)
+    p.add_argument("--replica-align", type=int, default=256,
+                   help="replica buffers start on multiples of this many bytes (1: packed at the odd stride L)")
     p.add_argument("--cpu-objects", type=int, default=8, help="objects in the CPU baseline sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-object HBM bytes per kernel from rocprofv3 PMC passes (tools/pmc_traffic.py)")
@@ -115,6 +117,17 @@ def cpu_baseline(k, n, size, nodes, count):
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
 
 
+def replica_stride(L, align):
+    """Distance between consecutive objects' replicas in one replica buffer.
+    The reference keeps every replica in its own heap buffer
+    (const_data_buffer), so each starts aligned; packing them at the odd
+    length L = 2T + 2 would start every odd object 2 bytes off a dword and
+    make every 1 KiB wave access straddle an extra 128-byte line (measured on
+    one box, 512 x 64 MiB at k=16: encode 2290 -> 2405, repair 1632 -> 1738
+    GiB/s with a 256-byte stride).  The bytes moved are the same."""
+    return -(-L // align) * align
+
+
 def kernel_names(k, n, nodes, size, L, objects):
     """Names of the kernels the C ABI dispatches for this workload."""
     import ctypes as C
@@ -160,7 +173,7 @@ def max_over_ranks(values, dist, device):
     return [float(x) for x in t.tolist()]
 
 
-def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, seed=1):
+def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, seed=1, align=256):
     """The production shape beside the metric (never in it): MIN_HORCRUX 32,
     GENERATE_HORCRUX 64 (dht_network.h:22-25) on the web client's 64 KiB
     blocks (web/src/store/vds_api.jsx:76).  Encode all 64 replicas of every
@@ -178,14 +191,15 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
     from vds_amd import _lib
     k, n, size = 32, 64, 65536
     L = chunk.replica_size(k, size)
+    Ls = replica_stride(L, align)
     inp = torch.empty(objects * size, dtype=torch.uint8, device=dev)
     chunk.fill_splitmix_device(inp, objects * size, SEED ^ 0x6C697665)
-    reps = torch.empty((n, objects * L), dtype=torch.uint8, device=dev)
+    reps = torch.empty((n, objects * Ls), dtype=torch.uint8, device=dev)
     out = torch.empty(objects * size, dtype=torch.uint8, device=dev)
     rep_ptrs = [reps[i].data_ptr() for i in range(n)]
 
     def enc():
-        chunk.encode_device(k, list(range(n)), inp, size, size, objects, rep_ptrs, L)
+        chunk.encode_device(k, list(range(n)), inp, size, size, objects, rep_ptrs, Ls)
 
     rng = np.random.default_rng(seed)
     lost = rng.random((objects, n)) < loss
@@ -193,7 +207,7 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
     objs = np.flatnonzero(ok)
     nodes = np.stack([np.flatnonzero(~lost[o])[:k] for o in objs]).astype(np.uint16)
     base = np.asarray(rep_ptrs, dtype=np.uint64)
-    chunk_ptrs = (base[nodes] + (objs.astype(np.uint64) * L)[:, None]).astype(np.uint64)
+    chunk_ptrs = (base[nodes] + (objs.astype(np.uint64) * Ls)[:, None]).astype(np.uint64)
     sizes = np.full(len(objs), L, dtype=np.uint64)
     pads = np.zeros(len(objs), dtype=np.uint16)
     outs = (np.uint64(out.data_ptr()) + objs.astype(np.uint64) * size).astype(np.uint64)
@@ -209,8 +223,8 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
     low_lost = lost[objs, :40]
     rg = np.flatnonzero(low_lost.any(axis=1))
     rg_targets = np.argmax(low_lost[rg], axis=1).astype(np.uint16)
-    rg_out = torch.empty(max(1, len(rg)) * L, dtype=torch.uint8, device=dev)
-    rg_outs = (np.uint64(rg_out.data_ptr()) + np.arange(len(rg), dtype=np.uint64) * L).astype(np.uint64)
+    rg_out = torch.empty(max(1, len(rg)) * Ls, dtype=torch.uint8, device=dev)
+    rg_outs = (np.uint64(rg_out.data_ptr()) + np.arange(len(rg), dtype=np.uint64) * Ls).astype(np.uint64)
     rg_nodes = np.ascontiguousarray(nodes[rg])
     rg_chunks = np.ascontiguousarray(chunk_ptrs[rg])
     rg_sizes = np.full(len(rg), L, dtype=np.uint64)
@@ -241,7 +255,7 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
     digests = torch.empty(n * objects * 32, dtype=torch.uint8, device=dev)
 
     def sha():
-        chunk.sha256_device(reps, L, L, n * objects, digests, stream)
+        chunk.sha256_device(reps, L, Ls, n * objects, digests, stream)
 
     with torch.cuda.stream(stream):
         enc_wall, enc_gpu = timed(enc)
@@ -252,10 +266,10 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
     idx = torch.from_numpy(objs).to(dev)
     assert torch.equal(out.view(objects, size)[idx], inp.view(objects, size)[idx]), "live restore differs"
     if len(rg):  # the regenerated replicas equal the encoded ones
-        want = torch.stack([reps[int(t), int(o) * L:(int(o) + 1) * L] for t, o in zip(rg_targets[:64], objs[rg[:64]])])
-        assert torch.equal(rg_out.view(-1, L)[:64], want), "live regenerate differs"
+        want = torch.stack([reps[int(t), int(o) * Ls:int(o) * Ls + L] for t, o in zip(rg_targets[:64], objs[rg[:64]])])
+        assert torch.equal(rg_out.view(-1, Ls)[:64, :L], want), "live regenerate differs"
     gib = lambda nbytes, t: round(nbytes / t / 2**30, 3) if t else None
-    res = {"shape": f"k={k}, n={n}, {objects} x 64 KiB objects; replica loss p={loss}; "
+    res = {"shape": f"k={k}, n={n}, {objects} x 64 KiB objects, replica stride {Ls} B; replica loss p={loss}; "
                     f"{len(objs)} restorable, {len(rg)} regenerated",
            "encode_GiBps": gib(objects * size, enc_gpu),
            "sha256_replicas_GiBps": gib(n * objects * L, sha_gpu),
@@ -267,9 +281,9 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
            "distinct_survivor_sets": int(len({tuple(r) for r in nodes.tolist()}))}
     # spot-check the digests against hashlib
     import hashlib
-    hb = reps.view(-1)[: 4 * L].cpu().numpy().tobytes()
+    hb = reps.view(-1)[: 4 * Ls].cpu().numpy().tobytes()
     dg = digests[: 4 * 32].cpu().numpy().tobytes()
-    assert all(hashlib.sha256(hb[i * L:(i + 1) * L]).digest() == dg[32 * i:32 * (i + 1)] for i in range(4)), "sha"
+    assert all(hashlib.sha256(hb[i * Ls:i * Ls + L]).digest() == dg[32 * i:32 * (i + 1)] for i in range(4)), "sha"
     del inp, reps, out, rg_out, digests
     return res
 
@@ -299,6 +313,7 @@ def main():
     n = k + m
     size = int(args.object_mib * (1 << 20))
     L = chunk.replica_size(k, size)
+    Ls = replica_stride(L, args.replica_align)
     if args.erase:
         erased = [int(x) for x in args.erase.split(",")]
     else:
@@ -309,13 +324,13 @@ def main():
     # ---- memory plan: inputs + all replicas + restored objects, resident in HBM
     objects = args.objects
     free, _total = torch.cuda.mem_get_info(dev)
-    per_obj = size + n * L + size
+    per_obj = size + n * Ls + size
     if objects * per_obj > 0.92 * free:
         objects = max(1, int(0.92 * free // per_obj))
     if world > 1:  # every rank runs the same count (weak scaling, value = world * objects)
         objects = int(-max_over_ranks([-objects], dist, dev)[0])
     inp = torch.empty(objects * size, dtype=torch.uint8, device=dev)
-    reps = torch.empty((n, objects * L), dtype=torch.uint8, device=dev)
+    reps = torch.empty((n, objects * Ls), dtype=torch.uint8, device=dev)
     restored = torch.empty(objects * size, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     for i, oid in enumerate(owned_objects(rank, world, objects)):
@@ -327,10 +342,10 @@ def main():
     padding = size % (2 * k)
 
     def encode():
-        chunk.encode_device(k, list(range(n)), inp, size, size, objects, rep_ptrs, L)
+        chunk.encode_device(k, list(range(n)), inp, size, size, objects, rep_ptrs, Ls)
 
     def repair():
-        chunk.restore_device(k, nodes, chunk_ptrs, L, L, padding, objects, restored, size)
+        chunk.restore_device(k, nodes, chunk_ptrs, L, Ls, padding, objects, restored, size)
 
     for _ in range(args.warmup):
         encode()
@@ -367,8 +382,8 @@ def main():
     if regen_out is not None and len(erased) == m:
         # written over the erased replicas' own buffers: same bytes, same place
         def regenerate():
-            chunk.regenerate_device(k, nodes, chunk_ptrs, L, L, objects, erased,
-                                    [reps[e].data_ptr() for e in erased], L)
+            chunk.regenerate_device(k, nodes, chunk_ptrs, L, Ls, objects, erased,
+                                    [reps[e].data_ptr() for e in erased], Ls)
         regenerate()
         torch.cuda.synchronize(dev)
         r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -387,11 +402,11 @@ def main():
     # Replica names, also beside the metric: SHA-256 of
     # every replica of the batch, one lane per replica (reps is [n][objects][L]).
     digests = torch.empty((n * objects, 32), dtype=torch.uint8, device=dev)
-    chunk.sha256_device(reps, L, L, n * objects, digests)
+    chunk.sha256_device(reps, L, Ls, n * objects, digests)
     torch.cuda.synchronize(dev)
     h0, h1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     h0.record(stream)
-    chunk.sha256_device(reps, L, L, n * objects, digests)
+    chunk.sha256_device(reps, L, Ls, n * objects, digests)
     h1.record(stream)
     torch.cuda.synchronize(dev)
     sha_ms = h0.elapsed_time(h1)
@@ -416,7 +431,8 @@ def main():
     if not args.no_live:
         del inp, restored, reps, digests, regen_out
         torch.cuda.empty_cache()
-        live = live_shape(torch, chunk, dev, torch.cuda.Stream(dev), args.live_objects, args.steps, args.warmup)
+        live = live_shape(torch, chunk, dev, torch.cuda.Stream(dev), args.live_objects, args.steps, args.warmup,
+                          align=args.replica_align)
 
     result = {
         "metric": "device-resident encode+repair GiB/s, k=16 m=4 64 MiB stripes, 1/2/4/8 GPU",
@@ -434,7 +450,7 @@ def main():
         "config": {"workload": f"k={k},m={m} encode of all {n} replicas + repair from {len(nodes)} "
                                f"(erased {erased}), {objects} x {size >> 20} MiB objects per GPU",
                    "k": k, "m": m, "objects_per_gpu": objects, "object_bytes": size,
-                   "erased": erased, "parallelism": f"objects round-robin over {world} GPU(s), no collective"},
+                   "erased": erased, "replica_bytes": L, "replica_stride": Ls, "parallelism": f"objects round-robin over {world} GPU(s), no collective"},
         "encode_GiBps": round(world * objects * size / (enc_ms * 1e-3) / 2**30, 3),
         "repair_GiBps": round(world * objects * size / (rep_ms * 1e-3) / 2**30, 3),
         "encode_ms": round(enc_ms, 3),

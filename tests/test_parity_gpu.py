@@ -140,6 +140,37 @@ def test_fast_equals_generic_path(ec):
         assert torch.equal(fast[r], gen[i])
 
 
+@pytest.mark.parametrize("k,align", [(16, 256), (32, 4096)])
+def test_bench_layout_aligned_replica_stride(ec, k, align):
+    """bench.py's layout: replica buffers [n][objects][Ls] with the replica
+    stride Ls = L rounded up to `align` (every replica starts aligned, as the
+    reference's own heap buffers do).  Every replica equals the oracle's,
+    the gaps stay untouched, and the syndrome restore from the survivors at
+    chunk stride Ls gives back the objects."""
+    import torch
+    from vds_amd import chunk
+    n, size, count = k + k // 4, 1 << 20, 3
+    L = chunk.replica_size(k, size)
+    Ls = -(-L // align) * align
+    t = torch.empty(size * count, dtype=torch.uint8, device="cuda")
+    for o in range(count):
+        chunk.fill_splitmix_device(t[o * size:], size, SEED + 1300 + o)
+    reps = torch.zeros((n, count * Ls), dtype=torch.uint8, device="cuda")
+    chunk.encode_device(k, list(range(n)), t, size, size, count, [reps[i].data_ptr() for i in range(n)], Ls)
+    erased = list(range(0, n, 5))[: n - k]
+    nodes = [r for r in range(n) if r not in erased]
+    out = torch.empty(size * count, dtype=torch.uint8, device="cuda")
+    chunk.restore_device(k, nodes, [reps[r].data_ptr() for r in nodes], L, Ls, size % (2 * k), count, out, size)
+    torch.cuda.synchronize()
+    host = reps.view(n, count, Ls).cpu().numpy()
+    for o in range(count):
+        d = O.splitmix(SEED + 1300 + o, size)
+        for r in range(n):
+            assert np.array_equal(host[r, o, :L], O.encode(k, r, d)), f"object {o} replica {r}"
+            assert not host[r, o, L:].any()
+        assert np.array_equal(out[o * size:(o + 1) * size].cpu().numpy(), d)
+
+
 def test_batched_objects_with_strides(ec):
     import torch
     k, n, size, count = 16, 20, 2 * 65536 + 1000, 5

@@ -18,20 +18,22 @@ p.add_argument("--iters", type=int, default=5)
 p.add_argument("--tag", default=os.path.basename(os.environ.get("VDS_EC_LIB", "default")))
 p.add_argument("--k", type=int, default=16, choices=(16, 32))
 p.add_argument("--check", action="store_true", help="compare the restored objects with the input")
+p.add_argument("--align", type=int, default=1, help="replica stride rounded up to this many bytes")
 a = p.parse_args()
 k, size = a.k, 64 << 20
 n = k + k // 4
 L = chunk.replica_size(k, size)
+Ls = -(-L // a.align) * a.align  # replica stride
 inp = torch.empty(a.objects * size, dtype=torch.uint8, device="cuda")
-reps = torch.empty((n, a.objects * L), dtype=torch.uint8, device="cuda")
+reps = torch.empty((n, a.objects * Ls), dtype=torch.uint8, device="cuda")
 out = torch.empty(a.objects * size, dtype=torch.uint8, device="cuda")
 for i in range(a.objects):
     chunk.fill_splitmix_device(inp[i * size:], size, 0x7664730000000000 + i)
 nodes = [r for r in range(n) if r % 5 != 0 or r >= 5 * (n - k)]  # erase 0, 5, 10, ..
 rp = [reps[i].data_ptr() for i in range(n)]
 cp = [reps[r].data_ptr() for r in nodes]
-enc = lambda: chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, rp, L)  # noqa: E731
-rep = lambda: chunk.restore_device(k, nodes, cp, L, L, size % (2 * k), a.objects, out, size)  # noqa: E731
+enc = lambda: chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, rp, Ls)  # noqa: E731
+rep = lambda: chunk.restore_device(k, nodes, cp, L, Ls, size % (2 * k), a.objects, out, size)  # noqa: E731
 enc()
 rep()
 torch.cuda.synchronize()
@@ -48,5 +50,5 @@ for name, f in (("encode", enc), ("repair", rep)):
 ok = ""
 if a.check:
     ok = " check " + ("ok" if torch.equal(out, inp) else "MISMATCH")
-print(f"{a.tag} k={k}: encode {res['encode'][0]:.3f} ms ({res['encode'][1]:.1f} GiB/s)  "
+print(f"{a.tag} k={k} align={a.align}: encode {res['encode'][0]:.3f} ms ({res['encode'][1]:.1f} GiB/s)  "
       f"repair {res['repair'][0]:.3f} ms ({res['repair'][1]:.1f} GiB/s){ok}", flush=True)

@@ -17,24 +17,26 @@ p.add_argument("--m", type=int, default=4)
 p.add_argument("--objects", type=int, default=64)
 p.add_argument("--iters", type=int, default=3)
 p.add_argument("--only", default="")
+p.add_argument("--replica-align", type=int, default=256, help="replica stride alignment (bench.py's default)")
 a = p.parse_args()
 k, n = a.k, a.k + a.m
 size = 64 << 20
 L = chunk.replica_size(k, size)
+Ls = -(-L // a.replica_align) * a.replica_align
 inp = torch.empty(a.objects * size, dtype=torch.uint8, device="cuda")
-reps = torch.empty((n, a.objects * L), dtype=torch.uint8, device="cuda")
+reps = torch.empty((n, a.objects * Ls), dtype=torch.uint8, device="cuda")
 out = torch.empty(a.objects * size, dtype=torch.uint8, device="cuda")
 for i in range(a.objects):
     chunk.fill_splitmix_device(inp[i * size:], size, 0x7664730000000000 + i)
 erased = list(range(0, n, n // a.m))[: a.m]
 nodes = [r for r in range(n) if r not in erased]
 rp = [reps[i].data_ptr() for i in range(n)]
-chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, rp, L)
+chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, rp, Ls)
 for _ in range(a.iters):
     if a.only != "restore":
-        chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, rp, L)
+        chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, rp, Ls)
     if a.only != "encode":
-        chunk.restore_device(k, nodes, [reps[r].data_ptr() for r in nodes], L, L, size % (2 * k), a.objects, out, size)
+        chunk.restore_device(k, nodes, [reps[r].data_ptr() for r in nodes], L, Ls, size % (2 * k), a.objects, out, size)
 torch.cuda.synchronize()
 assert torch.equal(out[:size], inp[:size]) or a.only == "encode"
 print("ok", k, n, a.objects)

@@ -43,6 +43,7 @@ struct SynShape {
   // conflict-free ds_{read,write}_b128 (byte (p/4)*1024 + lane*16 + 4*(p%4))
   static constexpr int kLdsBytes = N * 16 * 64 * 4;
   static constexpr int kWavesPerSimd = (160 * 1024 / kLdsBytes) * WV / 4;
+  static constexpr bool kPrio = 160 * 1024 / kLdsBytes >= 2;  // phase priorities (syn_prio)
   static_assert(K % WV == 0 && kM <= WV, "survivor loads and erased slots must map onto waves");
   static_assert(kSynRows == 16 && kM == WV, "scatter recovery needs one whole syndrome per wave");
   static_assert(kCells == 2 || kCells == 4, "row split must be b128 / word-group aligned");
@@ -59,6 +60,21 @@ struct SynShape {
 #ifndef VDS_DIAG_STAMPS
 #define VDS_DIAG_STAMPS 0
 #endif
+
+// Wave priority by phase when two workgroups share a CU (k = 16).  Their
+// phases drift apart; the workgroup in stage 1 (survivors -> LDS planes) and
+// stage A runs at priority 1, and the one transposing and staging its output
+// at 2, so the other workgroup's long XOR programs fill the gaps instead of
+// delaying the phases that end in a barrier of all four waves.  Same-box A/B,
+// 512 x 64 MiB: repair 18.65 -> 16.54-16.59 ms (+12%), again on a second box
+// 19.0-19.25 -> 16.9-17.0 ms.  Also measured: priority on the copy-out stores
+// (neutral), on stage 1 alone (+1.6%), staging alone (+0.5%), the syndrome
+// programs or stage B or C as well (less gain; every phase at 1 is the
+// default again).  One workgroup per CU (k = 32): neutral, not used.
+template <int PRIO, bool ON>
+__device__ __forceinline__ void syn_prio() {
+  if constexpr (ON) __builtin_amdgcn_s_setprio(PRIO);
+}
 
 #if VDS_DIAG_STAMPS
 constexpr int kStampPhases = 20;
@@ -189,9 +205,12 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
   constexpr int kPairs = (K / 2) / WV;           // stage-A pairs per wave
   constexpr int kHalfCells = P::kHalfRows / 16;  // stage-B cells per wave
   constexpr int kParts = WV / 2;                 // waves per half-size polynomial
+  constexpr bool kPrio = SynShape<K, N, WV>::kPrio;
   if constexpr (W < WV) {
     if (wave != W) return syn_interp_gm<K, N, WV, W + 1>(wave, L, cells, st);
+    syn_prio<1, kPrio>();
     syn_gm_stage_a<W, kPairs>(L);
+    syn_prio<0, kPrio>();
     st.mark(7);
     __syncthreads();
     st.mark(8);
@@ -305,6 +324,7 @@ __global__ __launch_bounds__((SynShape<K, N, WV>::kThreads), (SynShape<K, N, WV>
 void k_restore_syn(SynRestoreArgs a) {
   using S = SynShape<K, N, WV>;
   using P = typename S::P;
+  constexpr bool kPrio = S::kPrio;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -417,6 +437,7 @@ void k_restore_syn(SynRestoreArgs a) {
     auto erased_of = [&](int m) -> int { return (int)s_ld_u8(BATCH ? pl->erased : a.erased, m); };
     const int my_erased = wave < S::kM ? erased_of(wave) : 0;
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
+    syn_prio<1, kPrio>();
     {
       if (wave < S::kM) {
         const u32x4 z = {0u, 0u, 0u, 0u};
@@ -437,6 +458,7 @@ void k_restore_syn(SynRestoreArgs a) {
         syn_put_point(L, (int)s_ld_u8(BATCH ? pl->point : a.point, wave * S::kLoadPer + s), Pl);
       }
     }
+    syn_prio<0, kPrio>();
     st.mark(0);
     __syncthreads();
     st.mark(1);
@@ -599,6 +621,7 @@ void k_restore_syn(SynRestoreArgs a) {
         // wave-instruction (no partial lines).
         static_assert(S::kCells == 4, "one ds_write_b64 = the wave's 4 cells of a stripe");
         static_assert(2048 * 32 + 256 * 8 <= S::kLdsBytes, "staging layout is for 32-byte stripes");
+        syn_prio<2, kPrio>();
         uint32_t rows[2][32];
 #pragma unroll
         for (int g = 0; g < kGroups; ++g) {
@@ -619,6 +642,7 @@ void k_restore_syn(SynRestoreArgs a) {
           *(__attribute__((address_space(3))) u32x2 *)(w0 + (slot >> 3) * 16896 + (slot & 7) * 32) =
               u32x2{rows[0][pi], rows[1][pi]};
         }
+        syn_prio<0, kPrio>();
         st.mark(15);
         if (BATCH) prefetch(tile + t_step);  // (batch: the staged rows are dead; room for the survivors)
         __syncthreads();

@@ -70,7 +70,8 @@ struct SynShape {
 // 19.0-19.25 -> 16.9-17.0 ms.  Also measured: priority on the copy-out stores
 // (neutral), on stage 1 alone (+1.6%), staging alone (+0.5%), the syndrome
 // programs or stage B or C as well (less gain; every phase at 1 is the
-// default again).  One workgroup per CU (k = 32): neutral, not used.
+// default again); stage C at 1 or every level one higher (1 -> 2, 2 -> 3):
+// within 1%.  One workgroup per CU (k = 32): neutral, not used.
 template <int PRIO, bool ON>
 __device__ __forceinline__ void syn_prio() {
   if constexpr (ON) __builtin_amdgcn_s_setprio(PRIO);

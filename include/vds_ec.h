@@ -121,7 +121,12 @@ int vds_ec_restore8_device(uint8_t k, const uint8_t *nodes, const uint8_t *const
  * object o at chunks[j] + o*chunk_stride (HOST array of k device pointers,
  * chunk_size bytes = cells + BE16 trailer); replica targets[i] of object o is
  * written to outs[i] + o*out_stride (chunk_size bytes, trailer included).
- * Bytes equal chunk_generator(k, t).write(restore(...)) for valid replicas. */
+ * Bytes equal chunk_generator(k, t).write(restore(...)) -- the reference's
+ * route, restored object trimmed to E bytes, last stripe zero-padded, trailer
+ * E mod 2k -- for ANY survivors, codeword or not, whose first chunk's trailer
+ * p is at most 2k.  For p > 2k that route has no chunk_size-byte answer (it
+ * fails, or re-encodes to chunk_size + 2 bytes): the *_host forms return
+ * VDS_EC_ERESTORE, the device forms leave those objects' replicas unspecified. */
 int vds_ec_regenerate16_device(uint16_t k, const uint16_t *nodes, const uint8_t *const *chunks, uint64_t chunk_size,
                                uint64_t chunk_stride, uint32_t count, const uint16_t *targets, uint32_t ntargets,
                                uint8_t *const *outs, uint64_t out_stride, void *stream);
@@ -138,8 +143,9 @@ int vds_ec_regenerate16_device(uint16_t k, const uint16_t *nodes, const uint8_t 
  * targets[o*nt + i] (chunk_sizes[o] bytes, trailer included) to
  * outs[o*nt + i].  Objects whose survivors lie within the syndrome kernel's
  * points (k in {16, 32}, ids < k + k/4) share ONE launch; the others take
- * one launch each.  Every object is validated before anything is enqueued;
- * nothing synchronises.                                                      */
+ * one launch each.  Every object is validated before anything is enqueued
+ * (pointers, lengths, distinct ids: VDS_EC_ESINGULAR otherwise); nothing
+ * synchronises.  Regenerate bytes as vds_ec_regenerate16_device.             */
 int vds_ec_restore16_batch_device(uint16_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
                                   const uint64_t *chunk_sizes, const uint16_t *paddings, uint8_t *const *outs,
                                   unsigned flags, void *stream);

@@ -152,6 +152,110 @@ __global__ void k_regen_generic(RegenArgs a) {
   }
 }
 
+// ============================================================ regenerate tail
+// (RegenTailArgs, ec_internal.hpp): the last cell and the trailer of every
+// target replica as restore (trimmed to E) + re-encode writes them.
+
+__device__ __forceinline__ uint32_t be16_at(const uint8_t *p) { return (uint32_t)((p[0] << 8) | p[1]); }
+__device__ __forceinline__ void put_be16(uint8_t *p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 8);
+  p[1] = (uint8_t)(v & 0xFF);
+}
+// Decoded cell j of the last stripe as the reference's trimmed object holds
+// it: bytes [0, p) of the stripe kept (cell j = bytes 2j, 2j+1).
+__device__ __forceinline__ uint32_t trim_cell(uint32_t u, uint32_t j, uint32_t p) {
+  return 2 * j + 1 < p ? u : (2 * j + 1 == p ? (u & 0xFF00u) : 0u);
+}
+
+// One survivor set, host inverse: workgroup per object.  Threads j < J =
+// ceil(p/2) decode cell j of the last stripe (row j of V_S^{-1}), trimmed,
+// into LDS; then each target is a Horner over those J cells.
+__global__ void k_regen_tail(RegenTailArgs a) {
+  extern __shared__ uint16_t tail_cells[];
+  const uint64_t L = a.chunk_size, T = (L - 2) / 2;
+  for (uint32_t o = blockIdx.x; o < a.count; o += gridDim.x) {
+    auto chunk = [&](uint32_t j) {
+      return (a.chunk_table ? a.chunk_table[j] : a.chunk_ptr[j]) + (uint64_t)o * a.chunk_stride;
+    };
+    const uint32_t p = be16_at(chunk(0) + L - 2);
+    if (p > 2 * a.k) continue;  // no chunk_size-byte reference answer (ec_internal.hpp)
+    const uint32_t trailer = p == 2 * a.k ? 0u : p;
+    for (uint32_t i = threadIdx.x; i < a.nt; i += blockDim.x) put_be16(a.outs[i] + (uint64_t)o * a.out_stride + 2 * T, trailer);
+    if (p == 0 || p == 2 * a.k || T == 0) continue;  // nothing trimmed
+    const uint32_t J = (p + 1) / 2;
+    for (uint32_t j = threadIdx.x; j < J; j += blockDim.x) {
+      uint32_t u = 0;
+      for (uint32_t s = 0; s < a.k; ++s) {
+        const uint64_t e = (uint64_t)j * a.k + s;
+        const uint32_t coef = a.matrix_dev ? a.matrix_dev[e] : (a.matrix_inline[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+        u ^= gf16_mul(coef, be16_at(chunk(s) + 2 * (T - 1)));
+      }
+      tail_cells[j] = (uint16_t)trim_cell(u, j, p);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < a.nt; i += blockDim.x) {
+      uint32_t acc = 0;  // sum_j cell_j t^j (chunk.h:251-265)
+      for (uint32_t j = J; j-- > 0;) acc = gf16_mul(acc, a.targets[i]) ^ tail_cells[j];
+      put_be16(a.outs[i] + (uint64_t)o * a.out_stride + 2 * (T - 1), acc);
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off);
+  return v;
+}
+
+// Batched syndrome regenerate: one wave per object, its survivor set its own
+// (k <= 64), so the last stripe is interpolated here.  Lane s holds survivor
+// s (point a_s, cell c_s); with N(z) = prod_s (z + a_s) the decoded stripe is
+//   U(z) = sum_s w_s N(z) / (z + a_s),  w_s = c_s / prod_{j != s} (a_s + a_j)
+// (Lagrange; the unique polynomial through the survivors, as V_S^{-1} c).
+// The quotients q_s(z) = N(z) / (z + a_s) come out top coefficient first
+// (q_{s,m-1} = N_m + a_s q_{s,m}), so U_m = sum_s w_s q_{s,m} arrives in the
+// order a Horner evaluation of the targets consumes it.
+__global__ void k_regen_tail_batch(uint32_t k, uint32_t m, const SynBatchObj *objs, const SynBatchPlan *plans,
+                                   uint32_t count) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t waves = blockDim.x / 64;
+  for (uint32_t o = blockIdx.x * waves + (threadIdx.x >> 6); o < count; o += gridDim.x * waves) {
+    const SynBatchObj &d = objs[o];
+    const SynBatchPlan &pl = plans[d.plan];
+    const uint64_t L = d.chunk_len, T = (L - 2) / 2;
+    const uint32_t p = be16_at(d.chunks[d.first] + L - 2);
+    if (p > 2 * k) continue;
+    const uint32_t trailer = p == 2 * k ? 0u : p;
+    uint8_t *const rg = lane < (int)m ? d.regen[lane] : nullptr;
+    const uint32_t t = lane < (int)m ? pl.erased[lane] : 0u;
+    if (rg) put_be16(rg + 2 * T, trailer);
+    if (p == 0 || p == 2 * k || T == 0) continue;
+    const bool live = lane < (int)k;
+    const uint32_t as = live ? pl.point[lane] : 0u;
+    const uint32_t cs = live ? be16_at(d.chunks[lane] + 2 * (T - 1)) : 0u;
+    uint32_t Nm = lane == 0 ? 1u : 0u;  // lane m: coefficient m of N (N_k = 1 implicit)
+    uint32_t D = 1;
+    for (uint32_t j = 0; j < k; ++j) {
+      const uint32_t aj = __shfl(as, (int)j);
+      const uint32_t up = __shfl_up(Nm, 1);
+      Nm = (lane == 0 ? 0u : up) ^ gf16_mul(aj, Nm);
+      D = gf16_mul(D, j == (uint32_t)lane ? 1u : (as ^ aj));
+    }
+    const uint32_t w = live ? gf16_mul(cs, gf16_inv(D)) : 0u;
+    const uint32_t J = (p + 1) / 2;
+    uint32_t q = 1, acc = 0;
+    for (uint32_t mm = k; mm-- > 0;) {
+      if (mm < J) {  // (cells mm >= J are trimmed to zero: acc stays 0 above them)
+        const uint32_t u = trim_cell(wave_xor(gf16_mul(w, q)), mm, p);
+        acc = gf16_mul(acc, t) ^ u;
+      }
+      if (mm > 0) q = __shfl(Nm, (int)mm) ^ gf16_mul(as, q);
+    }
+    if (rg) put_be16(rg + 2 * (T - 1), acc);
+  }
+}
+
 // ============================================================== synthetic data
 
 __global__ void k_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed) {
@@ -207,6 +311,26 @@ hipError_t launch_regen_generic(const RegenArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_regen_generic<2>, dim3(grid), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(k_regen_generic<1>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_regen_tail(const RegenTailArgs &a, hipStream_t s) {
+  if (a.count == 0 || a.nt == 0 || a.chunk_size < 2) return hipSuccess;
+  // J = ceil(p / 2) <= 32768 cells (p is 16 bits)
+  const int lds = 2 * (int)(a.k < 32768u ? a.k : 32768u);
+  hipError_t e = ensure_lds_attr(&k_regen_tail, lds);
+  if (e != hipSuccess) return e;
+  const uint32_t grid = a.count < 4096u ? a.count : 4096u;
+  hipLaunchKernelGGL(k_regen_tail, dim3(grid), dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_regen_tail_batch(uint32_t k, uint32_t m, const SynBatchObj *objs, const SynBatchPlan *plans,
+                                   uint32_t count, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  if (k > 64 || m > (uint32_t)kMaxFastK / 4) return hipErrorInvalidValue;
+  const uint32_t waves = 4, grid = (count + waves - 1) / waves < 8192u ? (count + waves - 1) / waves : 8192u;
+  hipLaunchKernelGGL(k_regen_tail_batch, dim3(grid), dim3(64 * waves), 0, s, k, m, objs, plans, count);
   return hipGetLastError();
 }
 

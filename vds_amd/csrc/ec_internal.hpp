@@ -153,6 +153,8 @@ struct SynBatchObj {
   uint8_t *regen[kMaxFastK / 4];     // regenerate: replica erased[w] (nullptr: not requested)
   uint64_t out_len;                  // restore: E bytes to write
   uint64_t chunk_len;                // L = 2 T + 2 bytes of every survivor (and regenerated replica)
+  uint32_t plan;                     // its plan (the regenerate tail reads it)
+  uint32_t first;                    // plan position of the caller's chunk 0 (whose trailer restore reads)
 };
 struct SynBatchPlan {
   uint8_t erased[kMaxFastK / 4];
@@ -166,6 +168,42 @@ struct SynBatchTile {
   uint32_t trailer;     // regenerate: bit h = half h also copies its object's trailer cell
   uint32_t pad_[2];
 };
+
+// Reference-route tail of a regenerate.  The reference repairs a replica by
+// restoring the object -- trimmed to E bytes (chunk.h:415-419, 437-438) --
+// and re-encoding it: the last stripe zero-padded past E, trailer E mod 2k
+// (chunk.h:251-275; sync_process.cpp:313-335 -> dht_network_client.cpp:582-658).
+// The main regenerate kernels write P(t) of the untrimmed decode.  The two
+// agree on every cell but the last, and there only when the survivors are
+// not one codeword (a codeword's decode is already zero past E).  These
+// kernels rewrite, after the main ones on the same stream, the last cell and
+// the trailer of every target replica as the reference route writes them:
+// with p = the trailer of the caller's first survivor (the one restore reads,
+// chunk.h:408) and 0 < p < 2k, the decoded last stripe keeps bytes [0, p)
+// only.  p == 0 or p == 2k trim nothing (trailer 0 for both: E mod 2k).
+// p > 2k leaves the replica as the main kernels wrote it: the reference's
+// route either fails ("Fatal error", p > 4k) or writes a replica 2 bytes
+// longer than its survivors, so there is no chunk_size-byte answer; the host
+// entry points reject such survivors (VDS_EC_ERESTORE).
+struct RegenTailArgs {  // one survivor set, `count` objects at strides, any k
+  const uint8_t *chunk_ptr[kInlineChunks];
+  const uint8_t *const *chunk_table;  // used when k > kInlineChunks
+  uint64_t chunk_stride;
+  const uint16_t *matrix_dev;  // V_S^{-1} (k x k row-major) when k > kInlineMatrixK
+  uint32_t matrix_inline[kInlineMatrixK * kInlineMatrixK / 2];
+  uint64_t chunk_size;  // L = 2 T + 2
+  uint32_t k, count, nt;
+  uint16_t targets[kMaxLaunchReplicas];
+  uint8_t *outs[kMaxLaunchReplicas];
+  uint64_t out_stride;
+};
+hipError_t launch_regen_tail(const RegenTailArgs &a, hipStream_t s);
+// The batched k_restore_syn regenerate's objects objs[0..count) (device
+// tables of the batch launch; survivor points from their plans, targets the
+// plans' erased points with regen[w] set): the last stripe interpolated on
+// the device, one wave per object (k <= 64).
+hipError_t launch_regen_tail_batch(uint32_t k, uint32_t m, const SynBatchObj *objs, const SynBatchPlan *plans,
+                                   uint32_t count, hipStream_t s);
 
 hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s);
 bool has_restore_syn(uint32_t k, uint32_t n);

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <condition_variable>
 #include <cstdint>
 #include <atomic>
 #include <cstdio>
@@ -311,6 +312,7 @@ struct ParamSlot {
 struct ParamRing {
   static constexpr int kSlots = 16;
   std::mutex mu;
+  std::condition_variable freed;  // a slot was released
   ParamSlot slot[kSlots];
   unsigned next = 0;
   hipStream_t copy = nullptr;  // the copies run here, beside the caller's kernels
@@ -336,39 +338,48 @@ hipError_t param_acquire(size_t bytes, ParamSlot **out) {
   *out = nullptr;
   ParamRing *r = param_ring();
   if (!r) return hipErrorNoDevice;
-  std::lock_guard<std::mutex> g(r->mu);
-  // first choice: an idle slot already big enough whose readers are done
-  // (no allocation, no wait); else the next idle slot in rotation
-  ParamSlot *sp = nullptr;
-  for (int i = 0; i < ParamRing::kSlots && !sp; ++i) {
-    ParamSlot &c = r->slot[(r->next + i) % ParamRing::kSlots];
-    if (!c.busy && c.cap >= bytes && (!c.pending || hipEventQuery(c.ev) == hipSuccess)) sp = &c;
-  }
-  for (int i = 0; i < ParamRing::kSlots && !sp; ++i) {
-    ParamSlot &c = r->slot[r->next++ % ParamRing::kSlots];
-    if (!c.busy) sp = &c;
-  }
-  if (!sp) return hipErrorOutOfMemory;  // kSlots acquisitions in flight at once
+  std::unique_lock<std::mutex> g(r->mu);
   hipError_t e = hipSuccess;
   if (!r->copy && (e = hipStreamCreateWithFlags(&r->copy, hipStreamNonBlocking)) != hipSuccess) return e;
-  ParamSlot &sl = *sp;
-  if (sl.pending) {
-    e = hipEventSynchronize(sl.ev);
-    sl.pending = false;
-    if (e != hipSuccess) return e;
+  // first choice: an idle slot already big enough whose readers are done
+  // (no allocation, no wait); else the next idle slot in rotation; with all
+  // kSlots reserved by other threads, wait for a release
+  ParamSlot *sp = nullptr;
+  for (;;) {
+    for (int i = 0; i < ParamRing::kSlots && !sp; ++i) {
+      ParamSlot &c = r->slot[(r->next + i) % ParamRing::kSlots];
+      if (!c.busy && c.cap >= bytes && (!c.pending || hipEventQuery(c.ev) == hipSuccess)) sp = &c;
+    }
+    for (int i = 0; i < ParamRing::kSlots && !sp; ++i) {
+      ParamSlot &c = r->slot[r->next++ % ParamRing::kSlots];
+      if (!c.busy) sp = &c;
+    }
+    if (sp) break;
+    r->freed.wait(g);
   }
-  if (!sl.ev && (e = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming)) != hipSuccess) return e;
-  if (!sl.copied && (e = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming)) != hipSuccess) return e;
+  ParamSlot &sl = *sp;
+  sl.busy = true;  // reserved: from here on only this thread touches it
+  const bool pending = sl.pending;
+  sl.pending = false;
+  g.unlock();  // (the event wait and any allocation run outside the ring's lock)
+  auto fail = [&](hipError_t err) {
+    std::lock_guard<std::mutex> g2(r->mu);
+    sl.busy = false;
+    r->freed.notify_one();
+    return err;
+  };
+  if (pending && (e = hipEventSynchronize(sl.ev)) != hipSuccess) return fail(e);
+  if (!sl.ev && (e = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming)) != hipSuccess) return fail(e);
+  if (!sl.copied && (e = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if (bytes > sl.cap) {
     if (sl.h) (void)hipHostFree(sl.h);
     if (sl.d) (void)hipFree(sl.d);
     sl.h = sl.d = nullptr;
     sl.cap = 0;
-    if ((e = hipHostMalloc(&sl.h, bytes, 0)) != hipSuccess) return e;
-    if ((e = hipMalloc(&sl.d, bytes)) != hipSuccess) return e;
+    if ((e = hipHostMalloc(&sl.h, bytes, 0)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&sl.d, bytes)) != hipSuccess) return fail(e);
     sl.cap = bytes;
   }
-  sl.busy = true;
   *out = &sl;
   return hipSuccess;
 }
@@ -393,6 +404,7 @@ hipError_t param_release(ParamSlot *sl, hipStream_t s) {
   const hipError_t e = hipEventRecord(sl->ev, s);
   sl->pending = e == hipSuccess;
   sl->busy = false;
+  r->freed.notify_one();
   return e;
 }
 
@@ -722,10 +734,12 @@ int restore_host(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_t 
 // materialising the object: replica t = P(t) stripe by stripe, with P the
 // polynomial through the survivors.  This is what sync_process's repair does
 // with restore_async + save_data (sync_process.cpp:313-335,
-// dht_network_client.cpp:582-658) -- decode, then re-encode -- fused.  For a
-// valid codeword the bytes are identical to that route; for survivors that
-// are not one codeword they are P(t) for the polynomial through the survivors
-// (the reference would trim and zero-pad the decoded object first).
+// dht_network_client.cpp:582-658) -- decode, then re-encode -- fused.  The
+// main kernels write P(t) of the untrimmed decode; the tail kernel then
+// rewrites the last cell and the trailer as the route does (the decoded
+// object trimmed to E bytes, the last stripe zero-padded on re-encode), so
+// the bytes equal the reference's for any survivors, codeword or not
+// (RegenTailArgs, ec_internal.hpp).
 int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint8_t *const *chunks,
                       uint64_t chunk_size, uint64_t chunk_stride, uint32_t count, const uint16_t *targets,
                       uint32_t nt, uint8_t *const *outs, uint64_t out_stride, hipStream_t s) {
@@ -835,6 +849,8 @@ int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint
   std::vector<uint8_t> blob;
   const bool tmp_table = k > (uint32_t)kInlineChunks;
   const size_t off_table = tmp_table ? blob_append(blob, chunks, k) : SIZE_MAX;
+  // the tail's V_S^{-1} (regen_tail below)
+  const size_t off_inv = cb == 2 && k > (uint32_t)kInlineMatrixK ? blob_append(blob, inv.data(), inv.size()) : SIZE_MAX;
   std::vector<std::vector<uint16_t>> coef_blocks;
   std::vector<size_t> coef_off;
   for (uint32_t base = 0; base < nt; base += kMaxLaunchReplicas) {
@@ -876,6 +892,30 @@ int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint
       e = launch_regen_generic(ga, s);
     }
   }
+  // the reference route's last cell and trailer (trim to E, then re-encode),
+  // over what the kernels above wrote (same stream)
+  for (uint32_t base = 0; cb == 2 && base < nt && e == hipSuccess; base += kMaxLaunchReplicas) {
+    RegenTailArgs ta{};
+    if (tmp_table)
+      ta.chunk_table = reinterpret_cast<const uint8_t *const *>(dparam + off_table);
+    else
+      for (uint32_t j = 0; j < k; ++j) ta.chunk_ptr[j] = chunks[j];
+    ta.chunk_stride = chunk_stride;
+    if (off_inv != SIZE_MAX)
+      ta.matrix_dev = reinterpret_cast<const uint16_t *>(dparam + off_inv);
+    else
+      for (uint32_t i = 0; i < k * k; ++i) ta.matrix_inline[i >> 1] |= uint32_t(inv[i]) << (16 * (i & 1));
+    ta.chunk_size = chunk_size;
+    ta.k = k;
+    ta.count = count;
+    ta.nt = std::min<uint32_t>(nt - base, kMaxLaunchReplicas);
+    for (uint32_t i = 0; i < ta.nt; ++i) {
+      ta.targets[i] = targets[base + i];
+      ta.outs[i] = outs[base + i];
+    }
+    ta.out_stride = out_stride;
+    e = launch_regen_tail(ta, s);
+  }
   if (slot) {
     const hipError_t re = param_release(slot, s);
     if (e == hipSuccess) e = re;
@@ -891,6 +931,15 @@ int regenerate_host(unsigned cb, uint32_t k, const uint16_t *nodes, const uint8_
     if (!chunks[j]) return VDS_EC_EINVAL;
   for (uint32_t i = 0; i < nt; ++i)
     if (!outs[i]) return VDS_EC_EINVAL;
+  // The reference route restores first (chunk.h:402-444, with chunks[0]'s
+  // trailer p): a trailer it cannot restore with fails there ("Fatal
+  // error"), and p > 2k would re-encode to a replica longer than chunk_size.
+  if (cb == 2) {
+    const uint16_t p = (uint16_t)((chunks[0][chunk_size - 2] << 8) | chunks[0][chunk_size - 1]);
+    bool ok = true;
+    (void)restored_len(2, k, chunk_size, p, 0, &ok);
+    if (!ok || p > 2 * k) return VDS_EC_ERESTORE;
+  }
   int rc = device_ready();
   if (rc) return rc;
   if (nt == 0) return VDS_EC_OK;
@@ -923,6 +972,26 @@ int check_restore_args(uint32_t k, const Id *nodes, const uint8_t *const *chunks
   for (uint32_t j = 0; j < k; ++j)
     if (!chunks[j] && chunk_size) return VDS_EC_EINVAL;
   return VDS_EC_OK;
+}
+
+// The k replica ids of one object pairwise distinct (else V_S is singular).
+// The batch entry points check every object with this before anything is
+// enqueued, so a bad object fails the call without partial output.
+bool ids_distinct(uint32_t k, const uint16_t *nd) {
+  uint64_t seen = 0;
+  bool wide = false;
+  for (uint32_t j = 0; j < k; ++j) {
+    if (nd[j] >= 64) {
+      wide = true;
+      continue;
+    }
+    if ((seen >> nd[j]) & 1u) return false;
+    seen |= 1ull << nd[j];
+  }
+  if (!wide) return true;
+  std::vector<uint16_t> v(nd, nd + k);
+  std::sort(v.begin(), v.end());
+  return std::adjacent_find(v.begin(), v.end()) == v.end();
 }
 
 // ------------------------------------------------ batched device restore
@@ -1050,7 +1119,12 @@ struct SynBatchBuild {
     }
     SynBatchObj &d = objs[nobj++];
     uint32_t j = 0;
-    for (uint64_t b = seen; b; b &= b - 1) d.chunks[j++] = chunks[pos[__builtin_ctzll(b)]];
+    for (uint64_t b = seen; b; b &= b - 1, ++j) {
+      const uint32_t at = pos[__builtin_ctzll(b)];
+      d.chunks[j] = chunks[at];
+      if (at == 0) d.first = j;
+    }
+    d.plan = p;
     obj_plan.push_back(p);
     obj_halves.push_back((uint32_t)halves);
     return &d;
@@ -1096,6 +1170,9 @@ struct SynBatchBuild {
       sa.plans = reinterpret_cast<const SynBatchPlan *>(slot->d + o_plans);
       sa.total_tiles = (uint32_t)ntiles;
       e = launch_restore_syn_batch(k, n, sa, s, regen);
+      // regenerate: the reference route's last cell and trailer of every
+      // object (reads the same tables, so before the slot is released)
+      if (e == hipSuccess && regen) e = launch_regen_tail_batch(k, n - k, sa.objs, sa.plans, nobj, s);
     }
     const hipError_t re = param_release(slot, s);
     if (e == hipSuccess) e = re;
@@ -1121,6 +1198,7 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
     lens[o] = restored_len(2, k, chunk_sizes[o], paddings[o], flags, &ok);
     if (!ok) return VDS_EC_ERESTORE;
     if (lens[o] && !outs[o]) return VDS_EC_EINVAL;
+    if (lens[o] && !ids_distinct(k, nodes + (uint64_t)o * k)) return VDS_EC_ESINGULAR;
     const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);  // stripes that produce output
     halves += (need + kHalfStripes - 1) / kHalfStripes;
   }
@@ -1137,11 +1215,13 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
   uint8_t pos[64];
   for (uint32_t o = 0; o < count; ++o) {
     uint64_t seen = 0;
-    if (!syn || !syn_survivors(k, n, nodes + (uint64_t)o * k, &seen, pos)) {
+    const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);
+    // (SynBatchTile::stripe0 is 32-bit: objects past 2^32 stripes take the
+    // per-object path)
+    if (!syn || need > 0xFFFFFFFFull - kHalfStripes || !syn_survivors(k, n, nodes + (uint64_t)o * k, &seen, pos)) {
       fallback.push_back(o);
       continue;
     }
-    const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);
     if (need == 0) continue;
     const uint64_t h = (need + kHalfStripes - 1) / kHalfStripes;
     SynBatchObj *d = bb.add(seen, chunks + (uint64_t)o * k, pos, h);
@@ -1179,6 +1259,7 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
       if (!chunks[(uint64_t)o * k + j]) return VDS_EC_EINVAL;
     for (uint32_t i = 0; i < nt; ++i)
       if (!outs[(uint64_t)o * nt + i]) return VDS_EC_EINVAL;
+    if (!ids_distinct(k, nodes + (uint64_t)o * k)) return VDS_EC_ESINGULAR;
     const uint64_t T = (chunk_sizes[o] - 2) / 2;
     halves += T ? (T + kHalfStripes - 1) / kHalfStripes : 1;
   }
@@ -1195,7 +1276,8 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
   uint8_t pos[64];
   for (uint32_t o = 0; o < count; ++o) {
     uint64_t seen = 0;
-    bool ok = syn && syn_survivors(k, n, nodes + (uint64_t)o * k, &seen, pos);
+    const uint64_t T = (chunk_sizes[o] - 2) / 2;
+    bool ok = syn && T <= 0xFFFFFFFFull - kHalfStripes && syn_survivors(k, n, nodes + (uint64_t)o * k, &seen, pos);
     // every target must be an erased point, each at most once: wave w
     // recovers the w-th erased point (ascending)
     uint8_t *regen[kMaxFastK / 4] = {};
@@ -1210,7 +1292,6 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
       fallback.push_back(o);
       continue;
     }
-    const uint64_t T = (chunk_sizes[o] - 2) / 2;
     const uint64_t h = T ? (T + kHalfStripes - 1) / kHalfStripes : 1;
     SynBatchObj *d = bb.add(seen, chunks + (uint64_t)o * k, pos, h);
     if (!d) {
@@ -1471,6 +1552,7 @@ int restore_host_batch(uint32_t k, const uint16_t *nodes, const uint8_t *const *
     lens[o] = restored_len(2, k, cs, pads[o], flags, &ok);
     if (!ok) return VDS_EC_ERESTORE;
     if (lens[o] > out_sizes[o] || (lens[o] && !outs[o])) return VDS_EC_EINVAL;
+    if (lens[o] && !ids_distinct(k, nodes + (uint64_t)o * k)) return VDS_EC_ESINGULAR;
   }
   // the most a group's object can restore to: (chunk_size - 2) k plus a
   // corrupt trailer's excess, bounded by restored_len's own checks

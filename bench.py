@@ -173,20 +173,24 @@ def max_over_ranks(values, dist, device):
     return [float(x) for x in t.tolist()]
 
 
-def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, seed=1, align=256):
+def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02, 0.25), seed=1, align=256):
     """The production shape beside the metric (never in it): MIN_HORCRUX 32,
     GENERATE_HORCRUX 64 (dht_network.h:22-25) on the web client's 64 KiB
     blocks (web/src/store/vds_api.jsx:76).  Encode all 64 replicas of every
-    object (save_temp); then every replica is lost independently with
-    probability `loss`, each object is restored from the first 32 replicas
-    found (restore_async, dht_network_client.cpp:851-901) with ONE batched
-    call over all objects (vds_ec_restore16_batch_device), and one lost
-    replica of 0..39 per object is regenerated (sync_process's repair) with
-    vds_ec_regenerate16_batch_device.  Host times include the per-object
-    planning and table staging of the batched calls; max(steps, 10) timed
-    calls follow max(5, warmup) untimed ones (by then the process-wide erased-set plans
-    are solved and the pinned staging slots allocated, as in a running node)."""
-    import ctypes as C
+    object (save_temp) and name each by its SHA-256; then, per replica-loss
+    rate p, every replica is lost independently with probability p, each
+    object is restored from the first 32 replicas found (restore_async,
+    dht_network_client.cpp:851-901) with ONE batched call over all objects
+    (vds_ec_restore16_batch_device), and the first lost replica of every
+    object that lost one is regenerated (sync_process's repair) with
+    vds_ec_regenerate16_batch_device.  At p = 0.02 almost every survivor set
+    lies within replicas 0..39 (the syndrome kernel's points); at p = 0.25
+    most do not (the runtime-coefficient batch mode).  Host times include the
+    per-object planning and table staging of the batched calls; max(steps, 10)
+    timed calls follow max(5, warmup) untimed ones (by then the process-wide
+    erased-set plans are solved and the pinned staging slots allocated, as in
+    a running node).  Every restored object and every regenerated replica is
+    checked against the encoded bytes."""
     import numpy as np
     from vds_amd import _lib
     k, n, size = 32, 64, 65536
@@ -197,44 +201,8 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
     reps = torch.empty((n, objects * Ls), dtype=torch.uint8, device=dev)
     out = torch.empty(objects * size, dtype=torch.uint8, device=dev)
     rep_ptrs = [reps[i].data_ptr() for i in range(n)]
-
-    def enc():
-        chunk.encode_device(k, list(range(n)), inp, size, size, objects, rep_ptrs, Ls)
-
-    rng = np.random.default_rng(seed)
-    lost = rng.random((objects, n)) < loss
-    ok = (~lost).sum(axis=1) >= k
-    objs = np.flatnonzero(ok)
-    nodes = np.stack([np.flatnonzero(~lost[o])[:k] for o in objs]).astype(np.uint16)
-    base = np.asarray(rep_ptrs, dtype=np.uint64)
-    chunk_ptrs = (base[nodes] + (objs.astype(np.uint64) * Ls)[:, None]).astype(np.uint64)
-    sizes = np.full(len(objs), L, dtype=np.uint64)
-    pads = np.zeros(len(objs), dtype=np.uint16)
-    outs = (np.uint64(out.data_ptr()) + objs.astype(np.uint64) * size).astype(np.uint64)
     lib = _lib.lib()
     sp = stream.cuda_stream
-
-    def restore():
-        _lib.check(lib.vds_ec_restore16_batch_device(
-            k, len(objs), nodes.ctypes.data_as(_lib.u16p), chunk_ptrs.ctypes.data_as(_lib.vpp),
-            sizes.ctypes.data_as(_lib.u64p), pads.ctypes.data_as(_lib.u16p), outs.ctypes.data_as(_lib.vpp), 0, sp))
-
-    # regenerate: objects that lost a replica among 0..39, its first such id
-    low_lost = lost[objs, :40]
-    rg = np.flatnonzero(low_lost.any(axis=1))
-    rg_targets = np.argmax(low_lost[rg], axis=1).astype(np.uint16)
-    rg_out = torch.empty(max(1, len(rg)) * Ls, dtype=torch.uint8, device=dev)
-    rg_outs = (np.uint64(rg_out.data_ptr()) + np.arange(len(rg), dtype=np.uint64) * Ls).astype(np.uint64)
-    rg_nodes = np.ascontiguousarray(nodes[rg])
-    rg_chunks = np.ascontiguousarray(chunk_ptrs[rg])
-    rg_sizes = np.full(len(rg), L, dtype=np.uint64)
-
-    def regen():
-        _lib.check(lib.vds_ec_regenerate16_batch_device(
-            k, len(rg), rg_nodes.ctypes.data_as(_lib.u16p), rg_chunks.ctypes.data_as(_lib.vpp),
-            rg_sizes.ctypes.data_as(_lib.u64p), 1, rg_targets.ctypes.data_as(_lib.u16p),
-            rg_outs.ctypes.data_as(_lib.vpp), sp))
-
     reps_timed = max(steps, 10)  # (beside the metric: enough calls for a stable rate)
 
     def timed(fn):
@@ -250,6 +218,9 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / reps_timed, e0.elapsed_time(e1) / reps_timed * 1e-3
 
+    def enc():
+        chunk.encode_device(k, list(range(n)), inp, size, size, objects, rep_ptrs, Ls)
+
     # save_temp names every replica by its SHA-256 (dht_network_client.cpp:77-79):
     # one launch over all n x objects replicas (n * objects messages of L bytes)
     digests = torch.empty(n * objects * 32, dtype=torch.uint8, device=dev)
@@ -257,34 +228,79 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, loss=0.02, s
     def sha():
         chunk.sha256_device(reps, L, Ls, n * objects, digests, stream)
 
+    gib = lambda nbytes, t: round(nbytes / t / 2**30, 3) if t else None
     with torch.cuda.stream(stream):
         enc_wall, enc_gpu = timed(enc)
         sha_wall, sha_gpu = timed(sha)
-        rest_wall, rest_gpu = timed(restore)
-        regen_wall, regen_gpu = timed(regen) if len(rg) else (None, None)
     torch.cuda.synchronize(dev)
-    idx = torch.from_numpy(objs).to(dev)
-    assert torch.equal(out.view(objects, size)[idx], inp.view(objects, size)[idx]), "live restore differs"
-    if len(rg):  # the regenerated replicas equal the encoded ones
-        want = torch.stack([reps[int(t), int(o) * Ls:int(o) * Ls + L] for t, o in zip(rg_targets[:64], objs[rg[:64]])])
-        assert torch.equal(rg_out.view(-1, Ls)[:64, :L], want), "live regenerate differs"
-    gib = lambda nbytes, t: round(nbytes / t / 2**30, 3) if t else None
-    res = {"shape": f"k={k}, n={n}, {objects} x 64 KiB objects, replica stride {Ls} B; replica loss p={loss}; "
-                    f"{len(objs)} restorable, {len(rg)} regenerated",
+    res = {"shape": f"k={k}, n={n}, {objects} x 64 KiB objects, replica stride {Ls} B",
            "encode_GiBps": gib(objects * size, enc_gpu),
            "sha256_replicas_GiBps": gib(n * objects * L, sha_gpu),
-           "sha256_object_GiBps": gib(objects * size, sha_gpu),
-           "repair_GiBps": gib(len(objs) * size, rest_gpu),
-           "repair_host_GiBps": gib(len(objs) * size, rest_wall),
-           "regenerate_GiBps": gib(len(rg) * size, regen_gpu),
-           "regenerate_host_GiBps": gib(len(rg) * size, regen_wall),
-           "distinct_survivor_sets": int(len({tuple(r) for r in nodes.tolist()}))}
+           "sha256_object_GiBps": gib(objects * size, sha_gpu)}
     # spot-check the digests against hashlib
     import hashlib
     hb = reps.view(-1)[: 4 * Ls].cpu().numpy().tobytes()
     dg = digests[: 4 * 32].cpu().numpy().tobytes()
     assert all(hashlib.sha256(hb[i * Ls:i * Ls + L]).digest() == dg[32 * i:32 * (i + 1)] for i in range(4)), "sha"
-    del inp, reps, out, rg_out, digests
+    del digests
+    base = np.asarray(rep_ptrs, dtype=np.uint64)
+    reps2d = reps.view(n, objects, Ls)
+
+    for loss in losses:
+        rng = np.random.default_rng(seed)
+        lost = rng.random((objects, n)) < loss
+        objs = np.flatnonzero((~lost).sum(axis=1) >= k)
+        nodes = np.stack([np.flatnonzero(~lost[o])[:k] for o in objs]).astype(np.uint16)
+        chunk_ptrs = (base[nodes] + (objs.astype(np.uint64) * Ls)[:, None]).astype(np.uint64)
+        sizes = np.full(len(objs), L, dtype=np.uint64)
+        pads = np.zeros(len(objs), dtype=np.uint16)
+        outs = (np.uint64(out.data_ptr()) + objs.astype(np.uint64) * size).astype(np.uint64)
+
+        def restore():
+            _lib.check(lib.vds_ec_restore16_batch_device(
+                k, len(objs), nodes.ctypes.data_as(_lib.u16p), chunk_ptrs.ctypes.data_as(_lib.vpp),
+                sizes.ctypes.data_as(_lib.u64p), pads.ctypes.data_as(_lib.u16p), outs.ctypes.data_as(_lib.vpp), 0, sp))
+
+        # regenerate: the first lost replica of every object that lost one
+        rg = np.flatnonzero(lost[objs].any(axis=1))
+        rg_targets = np.argmax(lost[objs[rg]], axis=1).astype(np.uint16)
+        rg_out = torch.empty(max(1, len(rg)) * Ls, dtype=torch.uint8, device=dev)
+        rg_outs = (np.uint64(rg_out.data_ptr()) + np.arange(len(rg), dtype=np.uint64) * Ls).astype(np.uint64)
+        rg_nodes = np.ascontiguousarray(nodes[rg])
+        rg_chunks = np.ascontiguousarray(chunk_ptrs[rg])
+        rg_sizes = np.full(len(rg), L, dtype=np.uint64)
+
+        def regen():
+            _lib.check(lib.vds_ec_regenerate16_batch_device(
+                k, len(rg), rg_nodes.ctypes.data_as(_lib.u16p), rg_chunks.ctypes.data_as(_lib.vpp),
+                rg_sizes.ctypes.data_as(_lib.u64p), 1, rg_targets.ctypes.data_as(_lib.u16p),
+                rg_outs.ctypes.data_as(_lib.vpp), sp))
+
+        out.zero_()
+        rg_out.zero_()
+        with torch.cuda.stream(stream):
+            rest_wall, rest_gpu = timed(restore)
+            regen_wall, regen_gpu = timed(regen) if len(rg) else (None, None)
+        torch.cuda.synchronize(dev)
+        idx = torch.from_numpy(objs).to(dev)
+        assert torch.equal(out.view(objects, size)[idx], inp.view(objects, size)[idx]), f"live restore differs (p={loss})"
+        if len(rg):  # every regenerated replica equals the encoded one
+            want = reps2d[torch.from_numpy(rg_targets.astype(np.int64)).to(dev), torch.from_numpy(objs[rg]).to(dev), :L]
+            assert torch.equal(rg_out.view(-1, Ls)[:len(rg), :L], want), f"live regenerate differs (p={loss})"
+        syn_pts = int(((nodes < 40).all(axis=1)).sum())
+        leg = {"loss": loss, "restorable": int(len(objs)), "regenerated": int(len(rg)),
+               "repair_GiBps": gib(len(objs) * size, rest_gpu),
+               "repair_host_GiBps": gib(len(objs) * size, rest_wall),
+               "regenerate_GiBps": gib(len(rg) * size, regen_gpu),
+               "regenerate_host_GiBps": gib(len(rg) * size, regen_wall),
+               "distinct_survivor_sets": int(len({tuple(r) for r in nodes.tolist()})),
+               "survivors_within_0_39": syn_pts}
+        if loss == losses[0]:  # (the round-2 keys: the first loss rate)
+            res.update({kk: v for kk, v in leg.items() if kk not in ("loss",)})
+            res["shape"] += f"; replica loss p={loss}; {len(objs)} restorable, {len(rg)} regenerated"
+        res[f"loss_{loss}"] = leg
+        del rg_out
+    del inp, reps, out
     return res
 
 

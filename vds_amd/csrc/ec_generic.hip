@@ -216,23 +216,27 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
 // The quotients q_s(z) = N(z) / (z + a_s) come out top coefficient first
 // (q_{s,m-1} = N_m + a_s q_{s,m}), so U_m = sum_s w_s q_{s,m} arrives in the
 // order a Horner evaluation of the targets consumes it.
+// (rt: an RT object -- survivor points rt.spoint in slot order, targets
+// rt.epoint[0..ne); otherwise the plan's points and erased points)
 __global__ void k_regen_tail_batch(uint32_t k, uint32_t m, const SynBatchObj *objs, const SynBatchPlan *plans,
-                                   uint32_t count) {
+                                   uint32_t count, bool rt) {
   const int lane = threadIdx.x & 63;
   const uint32_t waves = blockDim.x / 64;
   for (uint32_t o = blockIdx.x * waves + (threadIdx.x >> 6); o < count; o += gridDim.x * waves) {
     const SynBatchObj &d = objs[o];
-    const SynBatchPlan &pl = plans[d.plan];
+    const uint8_t *const points = rt ? d.rt.spoint : plans[d.plan].point;
+    const uint8_t *const tpoints = rt ? d.rt.epoint : plans[d.plan].erased;
+    const uint32_t nt = rt ? d.rt.ne : m;
     const uint64_t L = d.chunk_len, T = (L - 2) / 2;
     const uint32_t p = be16_at(d.chunks[d.first] + L - 2);
     if (p > 2 * k) continue;
     const uint32_t trailer = p == 2 * k ? 0u : p;
-    uint8_t *const rg = lane < (int)m ? d.regen[lane] : nullptr;
-    const uint32_t t = lane < (int)m ? pl.erased[lane] : 0u;
+    uint8_t *const rg = lane < (int)nt ? d.regen[lane] : nullptr;
+    const uint32_t t = lane < (int)nt ? tpoints[lane] : 0u;
     if (rg) put_be16(rg + 2 * T, trailer);
     if (p == 0 || p == 2 * k || T == 0) continue;
     const bool live = lane < (int)k;
-    const uint32_t as = live ? pl.point[lane] : 0u;
+    const uint32_t as = live ? points[lane] : 0u;
     const uint32_t cs = live ? be16_at(d.chunks[lane] + 2 * (T - 1)) : 0u;
     uint32_t Nm = lane == 0 ? 1u : 0u;  // lane m: coefficient m of N (N_k = 1 implicit)
     uint32_t D = 1;
@@ -253,6 +257,45 @@ __global__ void k_regen_tail_batch(uint32_t k, uint32_t m, const SynBatchObj *ob
       if (mm > 0) q = __shfl(Nm, (int)mm) ^ gf16_mul(as, q);
     }
     if (rg) put_be16(rg + 2 * (T - 1), acc);
+  }
+}
+
+// RT coefficient rows (SynBatchRt): one wave per object, lane j = slot j
+// holding point a_j.  Row m, column j is the Lagrange basis polynomial of
+// slot j evaluated at t = epoint[m]:
+//   l_j(t) = prod_{i != j} (t + a_i) / D_j,  D_j = prod_{i != j} (a_j + a_i),
+// the numerator an exclusive product across the lanes (prefix x suffix
+// scans), so the only inversion is D_j's, once per slot.  t equal to a slot's
+// point gives the unit row, as it must.
+__global__ void k_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t waves = blockDim.x / 64;
+  for (uint32_t o = blockIdx.x * waves + (threadIdx.x >> 6); o < count; o += gridDim.x * waves) {
+    const SynBatchRt &r = objs[o].rt;
+    const uint32_t ne = r.ne;
+    if (ne == 0) continue;
+    const bool live = lane < (int)k;
+    const uint32_t a = live ? r.spoint[lane] : 0u;
+    uint32_t D = 1;
+    for (uint32_t j = 0; j < k; ++j) {
+      const uint32_t aj = __shfl(a, (int)j);
+      D = gf16_mul(D, j == (uint32_t)lane ? 1u : (a ^ aj));
+    }
+    const uint32_t invD = gf16_inv(D);
+    uint16_t *const out = const_cast<uint16_t *>(r.coef);
+    for (uint32_t m = 0; m < ne; ++m) {
+      const uint32_t f = live ? (r.epoint[m] ^ a) : 1u;
+      uint32_t pre = f, suf = f;  // inclusive prefix / suffix products over the lanes
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(pre, off), w = __shfl_down(suf, off);
+        if (lane >= off) pre = gf16_mul(pre, u);
+        if (lane + off < 64) suf = gf16_mul(suf, w);
+      }
+      const uint32_t before = __shfl_up(pre, 1), after = __shfl_down(suf, 1);
+      const uint32_t excl = gf16_mul(lane == 0 ? 1u : before, lane == 63 ? 1u : after);
+      if (live) out[(uint64_t)m * k + lane] = (uint16_t)gf16_mul(excl, invD);
+    }
   }
 }
 
@@ -330,7 +373,23 @@ hipError_t launch_regen_tail_batch(uint32_t k, uint32_t m, const SynBatchObj *ob
   if (count == 0) return hipSuccess;
   if (k > 64 || m > (uint32_t)kMaxFastK / 4) return hipErrorInvalidValue;
   const uint32_t waves = 4, grid = (count + waves - 1) / waves < 8192u ? (count + waves - 1) / waves : 8192u;
-  hipLaunchKernelGGL(k_regen_tail_batch, dim3(grid), dim3(64 * waves), 0, s, k, m, objs, plans, count);
+  hipLaunchKernelGGL(k_regen_tail_batch, dim3(grid), dim3(64 * waves), 0, s, k, m, objs, plans, count, false);
+  return hipGetLastError();
+}
+
+hipError_t launch_regen_tail_rt(uint32_t k, const SynBatchObj *objs, uint32_t count, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  if (k > 64) return hipErrorInvalidValue;
+  const uint32_t waves = 4, grid = (count + waves - 1) / waves < 8192u ? (count + waves - 1) / waves : 8192u;
+  hipLaunchKernelGGL(k_regen_tail_batch, dim3(grid), dim3(64 * waves), 0, s, k, 0u, objs, nullptr, count, true);
+  return hipGetLastError();
+}
+
+hipError_t launch_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  if (k > 64) return hipErrorInvalidValue;
+  const uint32_t waves = 4, grid = (count + waves - 1) / waves < 8192u ? (count + waves - 1) / waves : 8192u;
+  hipLaunchKernelGGL(k_rt_coefs, dim3(grid), dim3(64 * waves), 0, s, k, objs, count);
   return hipGetLastError();
 }
 

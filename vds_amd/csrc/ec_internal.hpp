@@ -147,14 +147,34 @@ struct RegenArgs {
 // tile's plan, so small objects (the live 64 KiB ones: 1024 stripes at
 // k = 32) pair up instead of filling half a tile each.
 constexpr uint32_t kHalfStripes = kTileStripes / 2;
+// Runtime-coefficient batch mode (k_restore_syn<..., RT>): survivor sets
+// outside the syndrome kernel's points -- the live n = 64 shape losing more
+// than k/4 of replicas 0..k+k/4-1, where restore_async's first k found reach
+// ids past k+k/4-1 (dht_network_client.cpp:851-901).  Slot j < K of an object
+// holds point j when that replica survives, else one of its survivors beyond
+// point K-1 ("borrowed" slot: point j itself is erased).  Output row m is a
+// combination of the K slots with the coefficients coef[m][0..K): restore:
+// the value at the erased point epoint[m] < K (then the fixed interpolation
+// from points 0..K-1 gives the object); regenerate: replica epoint[m].  The
+// rows are Lagrange over the slots' points, computed on the device
+// (launch_rt_coefs) from spoint / epoint.
+struct SynBatchRt {
+  const uint16_t *coef;       // ne x K, row-major, slot order (device)
+  uint64_t borrowed;          // bit j: slot j holds a survivor beyond K-1
+  uint32_t ne;                // rows
+  uint32_t pad_;
+  uint8_t epoint[kMaxFastK];  // point of output row m
+  uint8_t spoint[kMaxFastK];  // point held by slot j
+};
 struct SynBatchObj {
-  const uint8_t *chunks[kMaxFastK];  // survivor j = the chunk of plan point j (K used)
+  const uint8_t *chunks[kMaxFastK];  // survivor j = the chunk of plan point j (K used); RT: of slot j
   uint8_t *out;                      // restore: the object's bytes
-  uint8_t *regen[kMaxFastK / 4];     // regenerate: replica erased[w] (nullptr: not requested)
+  uint8_t *regen[kMaxFastK / 4];     // regenerate: replica erased[w] (nullptr: not requested); RT: of row w
   uint64_t out_len;                  // restore: E bytes to write
   uint64_t chunk_len;                // L = 2 T + 2 bytes of every survivor (and regenerated replica)
   uint32_t plan;                     // its plan (the regenerate tail reads it)
-  uint32_t first;                    // plan position of the caller's chunk 0 (whose trailer restore reads)
+  uint32_t first;                    // plan position (RT: slot) of the caller's chunk 0 (whose trailer restore reads)
+  SynBatchRt rt;                     // RT mode only
 };
 struct SynBatchPlan {
   uint8_t erased[kMaxFastK / 4];
@@ -164,9 +184,10 @@ struct SynBatchPlan {
 struct SynBatchTile {
   uint32_t obj[2];      // object of each half (an unused half: the batch's empty object)
   uint32_t stripe0[2];  // its first stripe
-  uint32_t plan;
+  uint32_t plan;        // (RT: unused)
   uint32_t trailer;     // regenerate: bit h = half h also copies its object's trailer cell
-  uint32_t pad_[2];
+  uint32_t nm;          // RT: rows of the tile = max ne over its halves
+  uint32_t pad_;
 };
 
 // Reference-route tail of a regenerate.  The reference repairs a replica by
@@ -204,6 +225,16 @@ hipError_t launch_regen_tail(const RegenTailArgs &a, hipStream_t s);
 // the device, one wave per object (k <= 64).
 hipError_t launch_regen_tail_batch(uint32_t k, uint32_t m, const SynBatchObj *objs, const SynBatchPlan *plans,
                                    uint32_t count, hipStream_t s);
+// The same for RT objects (survivor points rt.spoint, targets rt.epoint[0..ne)).
+hipError_t launch_regen_tail_rt(uint32_t k, const SynBatchObj *objs, uint32_t count, hipStream_t s);
+// RT coefficient rows of objs[0..count) (one wave per object, k <= 64): row m,
+// column j = l_j(epoint[m]), the Lagrange basis polynomial of slot j over the
+// slots' points spoint evaluated at epoint[m] -- the unique polynomial through
+// the k survivors, evaluated where it is needed.
+hipError_t launch_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count, hipStream_t s);
+// Batched RT restore / regenerate: a.objs / a.tiles / a.total_tiles set (every
+// object's rt filled, its coef rows computed); regenerate rows ne <= n - k.
+hipError_t launch_restore_rt_batch(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen);
 
 hipError_t launch_encode_generic(const GenericEncodeArgs &a, hipStream_t s);
 bool has_restore_syn(uint32_t k, uint32_t n);

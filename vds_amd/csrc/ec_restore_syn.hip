@@ -268,6 +268,35 @@ __device__ __forceinline__ void rec_pair(Plane16 &acc, const Plane16 &t, const P
       : VDS_RS_LIST(VDS_RS_A), VDS_RS_LIST(VDS_RS_B), [two] "s"(two)
       : "scc");
 }
+// RT mode: the same walk with a different coefficient in each half of the
+// tile.  After the stage-1 transpose, bits 0-7 and 16-23 of every plane word
+// hold half 0's stripes and bits 8-15, 24-31 half 1's (kRtH0 / kRtH1), so a
+// coefficient bit is a wave-uniform mask per bit -- 0, kRtH0, kRtH1 or all
+// ones -- and acc ^= (T & ma) ^ (T1 & mb) is one masked v_bitop3 per plane
+// and nonzero mask.  (Seven specialised arms per bit pair, as rec_pair's,
+// made the unrolled walk ~128 KiB of code: it thrashed the instruction cache,
+// 4x slower per tile.)  The mask is copied to a VGPR first: a v_bitop3
+// reading an SGPR issues at ~0.6 of the all-VGPR rate.
+constexpr uint32_t kRtH0 = 0x00FF00FFu, kRtH1 = 0xFF00FF00u;
+#define VDS_RD_MA(i) "v_bitop3_b32 %[c" #i "], %[c" #i "], %[a" #i "], %[tm] bitop3:0x78\n"
+#define VDS_RD_MB(i) "v_bitop3_b32 %[c" #i "], %[c" #i "], %[b" #i "], %[tm] bitop3:0x78\n"
+__device__ __forceinline__ void rec_dual(Plane16 &acc, const Plane16 &t, const Plane16 &t1, uint32_t ma, uint32_t mb) {
+  uint32_t tm;
+  asm volatile(
+      "s_cmp_eq_u32 %[ma], 0\n"
+      "s_cbranch_scc1 1f\n"
+      "v_mov_b32 %[tm], %[ma]\n" VDS_RS_SEQ(VDS_RD_MA)
+      "1:\n"
+      "s_cmp_eq_u32 %[mb], 0\n"
+      "s_cbranch_scc1 2f\n"
+      "v_mov_b32 %[tm], %[mb]\n" VDS_RS_SEQ(VDS_RD_MB)
+      "2:\n"
+      : VDS_RS_LIST(VDS_RS_C), [tm] "=&v"(tm)
+      : VDS_RS_LIST(VDS_RS_A), VDS_RS_LIST(VDS_RS_B), [ma] "s"(ma), [mb] "s"(mb)
+      : "scc");
+}
+#undef VDS_RD_MA
+#undef VDS_RD_MB
 #undef VDS_RS_C
 #undef VDS_RS_A
 #undef VDS_RS_B
@@ -276,6 +305,23 @@ __device__ __forceinline__ void rec_pair(Plane16 &acc, const Plane16 &t, const P
 #undef VDS_RS_XA
 #undef VDS_RS_XB
 #undef VDS_RS_X3
+
+// Coefficient idx of a wave-uniform uint16 table (s_load of its dword).
+__device__ __forceinline__ uint32_t s_ld_u16(const uint16_t *arr, uint32_t idx) {
+  const uint32_t w = s_ld(reinterpret_cast<const uint32_t *>(arr) + (idx >> 1));
+  return (w >> (16 * (idx & 1))) & 0xFFFFu;
+}
+
+// LDS XOR of a point's sixteen planes (this lane's 64 bytes) as eight
+// ds_xor_b64: planes 4g..4g+3 of point pt at byte (4 pt + g) 1 KiB + 16 lane.
+__device__ __forceinline__ void lds_xor_point(const SynLds &L, int pt, const Plane16 &v) {
+  __attribute__((address_space(3))) uint64_t *dst =
+      (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * pt);
+#pragma unroll
+  for (int h = 0; h < 8; ++h)
+    __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1), (uint64_t)v.p[2 * h] | ((uint64_t)v.p[2 * h + 1] << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // Batch mode: the last tile of an object may run past its bytes.  Loads
 // beyond `valid` bytes read zeros and stores beyond it write nothing (byte by
@@ -320,12 +366,21 @@ __device__ __forceinline__ void st16_guard(uint8_t *p, u32x4 v, int64_t valid) {
 // (q = 0, 1 and q = 2, 3 of the loads; waves 0..WV/2-1 and WV/2.. of the
 // copy-out) is a stripe range of its own object; a half that runs past its
 // object's bytes takes the guarded loads and stores.
-template <int K, int N, int WV, bool REGEN, bool BATCH>
+// RT (batch only): phase 2 is the runtime-coefficient combination of the
+// slots (SynBatchRt) instead of syndromes + recovery, so any k survivors of
+// any ids serve, a different set in each half of a tile: restore writes the
+// combinations into the borrowed slots' erased points and interpolates as
+// usual; regenerate accumulates row m in LDS slot K + m and stores it as
+// replica bytes.  Each wave combines the slots it loaded (registers) for
+// every row and adds its share with LDS XOR atomics, so the waves split the
+// work evenly whatever the rows.
+template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false>
 __global__ __launch_bounds__((SynShape<K, N, WV>::kThreads), (SynShape<K, N, WV>::kWavesPerSimd))
 void k_restore_syn(SynRestoreArgs a) {
   using S = SynShape<K, N, WV>;
   using P = typename S::P;
   constexpr bool kPrio = S::kPrio;
+  static_assert(!RT || BATCH, "RT is a batch mode");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -409,7 +464,9 @@ void k_restore_syn(SynRestoreArgs a) {
   // stores (REGEN has no interpolation and keeps the early issue)
   // (batch: the guarded loads and descriptor addresses would not fit beside
   // the programs either)
-  constexpr bool kLateLoad = (K == 32 || BATCH) && !REGEN;
+  // (RT: this wave's slots stay in registers through phase 2; the regenerate
+  // branch issues its prefetch there)
+  constexpr bool kLateLoad = ((K == 32 || BATCH) && !REGEN) || RT;
   const uint32_t t_step = tr.step;
   prefetch(tr.first);
   // vmcnt counts loads and stores together and retires them in issue order.
@@ -434,16 +491,24 @@ void k_restore_syn(SynRestoreArgs a) {
   for (uint32_t tile = tr.first; tile < tr.end; tile += t_step) {
     const uint32_t o = BATCH ? 0u : obj_of(tile);  // (non-batch)
     const uint64_t stripe0 = BATCH ? 0u : stripe0_of(tile);
-    const SynBatchPlan *pl = BATCH ? &a.plans[s_ld(&a.tiles[tile].plan)] : nullptr;
+    const SynBatchPlan *pl = (BATCH && !RT) ? &a.plans[s_ld(&a.tiles[tile].plan)] : nullptr;
     auto erased_of = [&](int m) -> int { return (int)s_ld_u8(BATCH ? pl->erased : a.erased, m); };
-    const int my_erased = wave < S::kM ? erased_of(wave) : 0;
+    // the LDS point this wave zeroes and (regenerate) stores: an erased point,
+    // or RT regenerate's row slot K + wave
+    const int my_erased = RT ? K + wave : (wave < S::kM ? erased_of(wave) : 0);
+    Plane16 Ps[RT ? S::kLoadPer : 1];  // RT: this wave's slots, kept for phase 2
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
     syn_prio<1, kPrio>();
     {
-      if (wave < S::kM) {
+      if (wave < S::kM && (!RT || REGEN)) {
         const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int g = 0; g < 4; ++g) L.put(4 * my_erased + g, z);
+      }
+      uint64_t bor[2] = {0, 0};  // RT restore: borrowed slots of each half
+      if constexpr (RT && !REGEN) {
+        bor[0] = s_ld(&half_obj(tile, 0).rt.borrowed);
+        bor[1] = s_ld(&half_obj(tile, 1).rt.borrowed);
       }
 #pragma unroll
       for (int s = 0; s < S::kLoadPer; ++s) {
@@ -456,13 +521,105 @@ void k_restore_syn(SynRestoreArgs a) {
         uint32_t Pl[16];
 #pragma unroll
         for (int b = 0; b < 16; ++b) Pl[b] = W[b ^ 8];
-        syn_put_point(L, (int)s_ld_u8(BATCH ? pl->point : a.point, wave * S::kLoadPer + s), Pl);
+        if constexpr (RT) {
+          const int j = wave * S::kLoadPer + s;
+#pragma unroll
+          for (int b = 0; b < 16; ++b) Ps[s].p[b] = Pl[b];
+          if constexpr (!REGEN) {
+            // slot j as point j: a borrowed half keeps zeros there (its
+            // erased point's value is added in phase 2)
+            const uint32_t keep = (((bor[0] >> j) & 1u) ? 0u : kRtH0) | (((bor[1] >> j) & 1u) ? 0u : kRtH1);
+            if (keep != 0xFFFFFFFFu)
+#pragma unroll
+              for (int b = 0; b < 16; ++b) Pl[b] &= keep;
+            syn_put_point(L, j, Pl);
+          }
+        } else {
+          syn_put_point(L, (int)s_ld_u8(BATCH ? pl->point : a.point, wave * S::kLoadPer + s), Pl);
+        }
       }
     }
     syn_prio<0, kPrio>();
     st.mark(0);
     __syncthreads();
     st.mark(1);
+    uint32_t rt_rows = 0;  // RT: rows of this tile
+    if constexpr (RT) {
+      // ---- 2'. row m of each half = sum_j coef[m][j] * slot j: every wave
+      // combines its own slots (Ps) for all rows, kMC rows per walk of each
+      // slot's x^b chain, and adds its share into the row's LDS point
+      // (restore: the half's erased point epoint[m], masked to the half when
+      // the two halves' points differ; regenerate: slot K + m)
+      const SynBatchObj &d0 = half_obj(tile, 0), &d1 = half_obj(tile, 1);
+      rt_rows = s_ld(&a.tiles[tile].nm);
+      const uint32_t ne0 = s_ld(&d0.rt.ne), ne1 = s_ld(&d1.rt.ne);
+      const uint16_t *cf0 = s_ld(&d0.rt.coef), *cf1 = s_ld(&d1.rt.coef);
+      uint32_t vh0, vh1;  // the half masks in VGPRs (for the scatter)
+      asm("v_mov_b32 %0, %1" : "=v"(vh0) : "i"(kRtH0));
+      asm("v_mov_b32 %0, %1" : "=v"(vh1) : "i"(kRtH1));
+      // two rows per walk of each slot's chain, the pairs in a rolled loop
+      // (code size: see rec_dual)
+      constexpr int kMC = 2;
+#pragma clang loop unroll(disable)
+      for (uint32_t m0 = 0; m0 < rt_rows; m0 += kMC) {
+        Plane16 ce[kMC];
+#pragma unroll
+        for (int m = 0; m < kMC; ++m) ce[m] = plane_zero();
+#pragma unroll
+        for (int s = 0; s < S::kLoadPer; ++s) {
+          const uint32_t j = wave * S::kLoadPer + s;
+          uint32_t c0[kMC], c1[kMC];
+#pragma unroll
+          for (int m = 0; m < kMC; ++m) {
+            c0[m] = m0 + m < ne0 ? s_ld_u16(cf0, (m0 + m) * K + j) : 0u;
+            c1[m] = m0 + m < ne1 ? s_ld_u16(cf1, (m0 + m) * K + j) : 0u;
+          }
+          // (one slot's chain at a time: interleaving the four independent
+          // chains would not fit beside the accumulators)
+          __builtin_amdgcn_sched_barrier(0);
+          Plane16 tt = Ps[s];
+#pragma unroll
+          for (int b = 0; b < 16; b += 2) {
+            __builtin_amdgcn_sched_barrier(0);
+            const Plane16 t1 = plane_mulx(tt);
+#pragma unroll
+            for (int m = 0; m < kMC; ++m) {
+              const uint32_t ma = (((c0[m] >> b) & 1u) ? kRtH0 : 0u) | (((c1[m] >> b) & 1u) ? kRtH1 : 0u);
+              const uint32_t mb = (((c0[m] >> (b + 1)) & 1u) ? kRtH0 : 0u) | (((c1[m] >> (b + 1)) & 1u) ? kRtH1 : 0u);
+              rec_dual(ce[m], tt, t1, ma, mb);
+            }
+            if (b < 14) tt = plane_mulx(t1);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < kMC; ++m) {
+          const uint32_t r = m0 + m;
+          if (r >= rt_rows) break;
+          if constexpr (REGEN) {
+            lds_xor_point(L, K + (int)r, ce[m]);
+          } else {
+            const int p0 = r < ne0 ? (int)s_ld_u8(d0.rt.epoint, (int)r) : -1;
+            const int p1 = r < ne1 ? (int)s_ld_u8(d1.rt.epoint, (int)r) : -1;
+            if (p0 >= 0 && p0 == p1) {
+              lds_xor_point(L, p0, ce[m]);
+            } else {
+              if (p0 >= 0) {
+                Plane16 v;
+#pragma unroll
+                for (int b = 0; b < 16; ++b) v.p[b] = ce[m].p[b] & vh0;
+                lds_xor_point(L, p0, v);
+              }
+              if (p1 >= 0) {
+                Plane16 v;
+#pragma unroll
+                for (int b = 0; b < 16; ++b) v.p[b] = ce[m].p[b] & vh1;
+                lds_xor_point(L, p1, v);
+              }
+            }
+          }
+        }
+      }
+    } else {
     // ---- 2. wave j holds syndrome S_j whole and scatters its share of every
     // recovered point, c_e[m] += R[m][j] S_j, into the erased slots (zero since
     // stage 1) with LDS XOR atomics: T = x^b S_j walks the coefficient bits
@@ -503,17 +660,10 @@ void k_restore_syn(SynRestoreArgs a) {
         if constexpr (kMC == S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
         st.mark(4);
 #pragma unroll
-        for (int m = 0; m < kMC; ++m) {
-          __attribute__((address_space(3))) uint64_t *dst =
-              (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * erased_of(m0 + m));
-#pragma unroll
-          for (int h = 0; h < 8; ++h)
-            __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1),
-                                   (uint64_t)ce[m].p[2 * h] | ((uint64_t)ce[m].p[2 * h + 1] << 32), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        for (int m = 0; m < kMC; ++m) lds_xor_point(L, erased_of(m0 + m), ce[m]);
       }
     }
+    }  // (phase 2)
     st.mark(5);
     __syncthreads();
     st.mark(6);
@@ -522,8 +672,10 @@ void k_restore_syn(SynRestoreArgs a) {
       // (P(e_w) stripe by stripe).  Undo the stage-1 transpose and store it as
       // big-endian cells, one 1 KiB store per wave-instruction; no
       // interpolation (fused "decode + re-encode" of sync_process.cpp:313-335).
+      // (RT: row w's slot K + w, for w < the tile's rows)
+      if constexpr (RT) prefetch(tile + t_step);
       if constexpr (BATCH) {
-        if (wave < S::kM) {
+        if (RT ? (uint32_t)wave < rt_rows : wave < S::kM) {
           uint32_t Pl[16], W[16];
           syn_get_point(L, my_erased, Pl);
 #pragma unroll
@@ -743,10 +895,10 @@ const uint16_t *restore_syn_weights(uint32_t k, uint32_t n) {
   return nullptr;
 }
 
-template <int K, int N, int WV, bool REGEN, bool BATCH = false>
+template <int K, int N, int WV, bool REGEN, bool BATCH = false, bool RT = false>
 static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) {
   using S = SynShape<K, N, WV>;
-  hipError_t e = ensure_lds_attr(&k_restore_syn<K, N, WV, REGEN, BATCH>, S::kLdsBytes);
+  hipError_t e = ensure_lds_attr(&k_restore_syn<K, N, WV, REGEN, BATCH, RT>, S::kLdsBytes);
   if (e != hipSuccess) return e;
   const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
   uint32_t grid = 256u * (blocks_per_cu > 0 ? blocks_per_cu : 1);
@@ -754,7 +906,7 @@ static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) 
   if (over) grid = over;
   if (grid > a.total_tiles) grid = a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_restore_syn<K, N, WV, REGEN, BATCH>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  hipLaunchKernelGGL((k_restore_syn<K, N, WV, REGEN, BATCH, RT>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
   return hipGetLastError();
 }
 
@@ -771,6 +923,16 @@ hipError_t launch_restore_syn_batch(uint32_t k, uint32_t n, const SynRestoreArgs
     return regen ? launch_restore_syn_kn<16, 20, 4, true, true>(a, s) : launch_restore_syn_kn<16, 20, 4, false, true>(a, s);
   if (k == 32 && n == 40)
     return regen ? launch_restore_syn_kn<32, 40, 8, true, true>(a, s) : launch_restore_syn_kn<32, 40, 8, false, true>(a, s);
+  return hipErrorNotSupported;
+}
+
+hipError_t launch_restore_rt_batch(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen) {
+  if (k == 16 && n == 20)
+    return regen ? launch_restore_syn_kn<16, 20, 4, true, true, true>(a, s)
+                 : launch_restore_syn_kn<16, 20, 4, false, true, true>(a, s);
+  if (k == 32 && n == 40)
+    return regen ? launch_restore_syn_kn<32, 40, 8, true, true, true>(a, s)
+                 : launch_restore_syn_kn<32, 40, 8, false, true, true>(a, s);
   return hipErrorNotSupported;
 }
 

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <array>
 #include <climits>
 #include <condition_variable>
 #include <cstdint>
@@ -18,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -1001,9 +1003,10 @@ bool ids_distinct(uint32_t k, const uint16_t *nd) {
 // repairs object by object, sync_process.cpp:313-335).  Objects whose
 // survivors lie within the syndrome kernel's points go to ONE launch of
 // k_restore_syn in batch mode over every half-tile (kHalfStripes stripes) of
-// every such object, the halves of one erased set paired into tiles; other
-// objects fall back to one restore_device / regenerate_device call each, on
-// the same stream.  Nothing synchronises.
+// every such object, the halves of one erased set paired into tiles; objects
+// of a compiled k whose survivors lie elsewhere go to ONE launch of its
+// runtime-coefficient (RT) mode; the rest fall back to one restore_device /
+// regenerate_device call each, on the same stream.  Nothing synchronises.
 //
 // An erased set's plan (the M x M solve) never changes, so solved plans are
 // kept process-wide: a repair loop meets the same few loss patterns again and
@@ -1052,22 +1055,148 @@ bool syn_plan(uint32_t k, uint32_t n, uint64_t seen, SynBatchPlan *out) {
   return true;
 }
 
-// Survivor set of one object as a bitmask over the syndrome kernel's points,
-// with pos[a] = the node-list index of point a; false when not eligible.
-inline bool syn_survivors(uint32_t k, uint32_t n, const uint16_t *nd, uint64_t *seen, uint8_t *pos) {
-  uint64_t m = 0;
-  for (uint32_t j = 0; j < k; ++j) {
-    const uint32_t a = nd[j];
-    if (a >= n || ((m >> a) & 1u)) return false;
-    m |= 1ull << a;
-    pos[a] = (uint8_t)j;
+// ------------------------------------------------------ host thread pool
+// The batch planners' per-object passes run over a few worker threads: the
+// live repair loop plans 16,384 objects per call, and one thread took longer
+// (3.3 ms) than the kernels it feeds.  Workers start once and wait for a job;
+// a caller that finds the pool busy (another thread's batch) runs its parts
+// inline.
+class HostPool {
+ public:
+  static HostPool &get() {
+    static HostPool *p = new HostPool();  // never freed: detached workers outlive every caller
+    return *p;
   }
-  *seen = m;
-  return true;
+  // fn(part) for every part in [0, parts), over the workers and the caller.
+  template <class F>
+  void run(unsigned parts, F &&fn) {
+    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+    if (parts <= 1 || !busy.owns_lock() || nworkers_ == 0) {
+      for (unsigned p = 0; p < parts; ++p) fn(p);
+      return;
+    }
+    auto job = std::make_shared<Job>();
+    job->fn = [&fn](unsigned p) { fn(p); };
+    job->parts = parts;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      cur_ = job;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work(*job);
+    std::unique_lock<std::mutex> g(job->m);
+    job->cv.wait(g, [&] { return job->done.load() == job->parts; });
+  }
+
+ private:
+  struct Job {
+    std::function<void(unsigned)> fn;
+    unsigned parts = 0;
+    std::atomic<unsigned> next{0}, done{0};
+    std::mutex m;
+    std::condition_variable cv;
+  };
+  HostPool() {
+    const unsigned hw = std::thread::hardware_concurrency();
+    nworkers_ = hw > 1 ? std::min(hw - 1, 7u) : 0u;
+    for (unsigned i = 0; i < nworkers_; ++i) std::thread([this] { loop(); }).detach();
+  }
+  static void work(Job &j) {
+    for (;;) {
+      const unsigned p = j.next.fetch_add(1);
+      if (p >= j.parts) return;
+      j.fn(p);
+      if (j.done.fetch_add(1) + 1 == j.parts) {
+        std::lock_guard<std::mutex> g(j.m);
+        j.cv.notify_all();
+      }
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+        j = cur_;
+      }
+      if (j) work(*j);
+    }
+  }
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_;
+  std::shared_ptr<Job> cur_;
+  uint64_t gen_ = 0;
+  unsigned nworkers_ = 0;
+};
+
+// fn(o0, o1) over [0, count) in ranges of at least kMinPer objects.
+template <class F>
+void parallel_objects(uint32_t count, F &&fn) {
+  constexpr uint32_t kMinPer = 1024;
+  const unsigned parts = std::min<uint32_t>(8, std::max<uint32_t>(1, count / kMinPer));
+  HostPool::get().run(parts, [&](unsigned p) {
+    fn((uint32_t)((uint64_t)count * p / parts), (uint32_t)((uint64_t)count * (p + 1) / parts));
+  });
 }
 
-// Host-side builder of one batched launch, written straight into a pinned
-// parameter slot: objs (and the empty object), then tiles, then plans.
+// The first failure of a parallel validation pass: the lowest object's.
+struct FirstError {
+  std::mutex mu;
+  uint32_t obj = UINT32_MAX;
+  int rc = VDS_EC_OK;
+  void note(uint32_t o, int r) {
+    std::lock_guard<std::mutex> g(mu);
+    if (o < obj) {
+      obj = o;
+      rc = r;
+    }
+  }
+};
+
+// Per-object facts of a batch call, from one parallel pass.  Routes:
+// kRouteSyn = survivors within the syndrome kernel's points (k_restore_syn
+// batch, by erased-set plan); kRouteRt = any other survivors of a compiled k
+// with ids < 256 (the RT batch: per-object coefficient rows); kRouteOne =
+// the rest (other k, cell arrays), one restore_device / regenerate_device
+// per object; kRouteSkip = nothing to write.
+enum : uint8_t { kRouteSkip, kRouteSyn, kRouteRt, kRouteOne };
+struct BatchObjInfo {
+  uint64_t seen;    // survivor ids below 64 as bits
+  uint32_t halves;  // half tiles (kHalfStripes stripes) of its output
+  uint16_t rows;    // RT rows: restore, its erased points below k; regenerate, its targets
+  uint8_t route;
+  uint8_t parts;    // RT descriptors (regenerate: rows in groups of at most n - k)
+};
+
+// The survivor ids of one object: those below 64 as bits, the largest; false
+// when two coincide (V_S singular).
+inline bool id_set(uint32_t k, const uint16_t *nd, uint64_t *seen, uint32_t *maxid) {
+  uint64_t m = 0;
+  uint32_t mx = 0;
+  bool wide = false;
+  for (uint32_t j = 0; j < k; ++j) {
+    const uint32_t a = nd[j];
+    mx = a > mx ? a : mx;
+    if (a >= 64) {
+      wide = true;
+    } else {
+      if ((m >> a) & 1u) return false;
+      m |= 1ull << a;
+    }
+  }
+  *seen = m;
+  *maxid = mx;
+  return !wide || ids_distinct(k, nd);
+}
+
+// Host-side builder of one k_restore_syn batch launch, written straight into
+// a pinned parameter slot: objs (and the empty object), then tiles, then
+// plans.  plan_of() (serial) resolves survivor sets to plans; fill() writes
+// descriptor i and may run on several threads for distinct i.
 struct SynBatchBuild {
   uint32_t k, n;
   ParamSlot *slot = nullptr;
@@ -1085,6 +1214,7 @@ struct SynBatchBuild {
   static size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
 
   hipError_t begin(uint32_t count, uint64_t halves) {
+    nobj = count;
     cap_objs = (size_t)count + 1;
     cap_tiles = (size_t)((halves + count + 1) / 2 + 1);  // pairs within each plan: <= (halves + plans) / 2
     cap_plans = count;
@@ -1092,8 +1222,8 @@ struct SynBatchBuild {
     o_plans = up16(o_tiles + cap_tiles * sizeof(SynBatchTile));
     hipError_t e = param_acquire(o_plans + cap_plans * sizeof(SynBatchPlan), &slot);
     if (e == hipSuccess) objs = reinterpret_cast<SynBatchObj *>(slot->h);
-    obj_plan.reserve(count);
-    obj_halves.reserve(count);
+    obj_plan.assign(count, 0);
+    obj_halves.assign(count, 0);
     unsigned bits = 4;
     while ((1ull << bits) < 2ull * count) ++bits;
     hkey.assign(1ull << bits, 0);
@@ -1101,41 +1231,42 @@ struct SynBatchBuild {
     hshift = 64 - bits;
     return e;
   }
-  // A new object of survivor set `seen`; nullptr if the set has no solve.
-  SynBatchObj *add(uint64_t seen, const uint8_t *const *chunks, const uint8_t *pos, uint64_t halves) {
+  // The plan of survivor set `seen` (UINT32_MAX: no solve; not for distinct points).
+  uint32_t plan_of(uint64_t seen) {
     const size_t mask = hkey.size() - 1;
     size_t i = (size_t)((seen * 0x9E3779B97F4A7C15ull) >> hshift);
     while (hkey[i] != 0 && hkey[i] != seen) i = (i + 1) & mask;
-    uint32_t p;
-    if (hkey[i] == seen) {
-      p = hval[i];
-    } else {
-      SynBatchPlan pl;
-      if (!syn_plan(k, n, seen, &pl)) return nullptr;
-      p = (uint32_t)plans.size();
-      plans.push_back(pl);
-      hkey[i] = seen;
-      hval[i] = p;
-    }
-    SynBatchObj &d = objs[nobj++];
+    if (hkey[i] == seen) return hval[i];
+    SynBatchPlan pl;
+    if (!syn_plan(k, n, seen, &pl)) return UINT32_MAX;
+    const uint32_t p = (uint32_t)plans.size();
+    plans.push_back(pl);
+    hkey[i] = seen;
+    hval[i] = p;
+    return p;
+  }
+  // Descriptor i: survivors in the plan's point order (ascending ids).
+  SynBatchObj &fill(uint32_t i, uint64_t seen, const uint16_t *nd, const uint8_t *const *chunks, uint32_t plan,
+                    uint32_t halves) {
+    uint8_t pos[64];
+    for (uint32_t j = 0; j < k; ++j) pos[nd[j]] = (uint8_t)j;
+    SynBatchObj &d = objs[i];
     uint32_t j = 0;
     for (uint64_t b = seen; b; b &= b - 1, ++j) {
       const uint32_t at = pos[__builtin_ctzll(b)];
       d.chunks[j] = chunks[at];
       if (at == 0) d.first = j;
     }
-    d.plan = p;
-    obj_plan.push_back(p);
-    obj_halves.push_back((uint32_t)halves);
-    return &d;
+    d.plan = plan;
+    obj_plan[i] = plan;
+    obj_halves[i] = halves;
+    return d;
   }
   // Pair the halves of each plan into tiles, stage and launch (regenerate:
-  // the last half of every object also copies its trailer cell).
+  // the last half of every object also copies its trailer cell, and the tail
+  // kernel then writes the reference route's last cell and trailer).
   int launch(bool regen, hipStream_t s) {
-    if (nobj == 0) {
-      const hipError_t e = param_release(slot, s);
-      return hip_status(e);
-    }
+    if (nobj == 0) return hip_status(param_release(slot, s));
     const uint32_t empty = nobj;
     std::memset(&objs[empty], 0, sizeof(SynBatchObj));
     std::vector<uint64_t> first(plans.size() + 1, 0);  // tile offset of each plan
@@ -1148,9 +1279,9 @@ struct SynBatchBuild {
       return VDS_EC_EINVAL;
     }
     SynBatchTile *tiles = reinterpret_cast<SynBatchTile *>(slot->h + o_tiles);
-    for (uint64_t t = 0; t < ntiles; ++t) tiles[t] = SynBatchTile{{empty, empty}, {0, 0}, 0, 0, {0, 0}};
     for (size_t p = 0; p < plans.size(); ++p)
-      for (uint64_t t = first[p]; t < first[p + 1]; ++t) tiles[t].plan = (uint32_t)p;
+      for (uint64_t t = first[p]; t < first[p + 1]; ++t)
+        tiles[t] = SynBatchTile{{empty, empty}, {0, 0}, (uint32_t)p, 0, 0, 0};
     for (uint32_t o = 0; o < nobj; ++o) {
       const uint32_t p = obj_plan[o];
       for (uint32_t h = 0; h < obj_halves[o]; ++h) {
@@ -1170,8 +1301,7 @@ struct SynBatchBuild {
       sa.plans = reinterpret_cast<const SynBatchPlan *>(slot->d + o_plans);
       sa.total_tiles = (uint32_t)ntiles;
       e = launch_restore_syn_batch(k, n, sa, s, regen);
-      // regenerate: the reference route's last cell and trailer of every
-      // object (reads the same tables, so before the slot is released)
+      // (reads the same tables, so before the slot is released)
       if (e == hipSuccess && regen) e = launch_regen_tail_batch(k, n - k, sa.objs, sa.plans, nobj, s);
     }
     const hipError_t re = param_release(slot, s);
@@ -1183,60 +1313,260 @@ struct SynBatchBuild {
   }
 };
 
+// Host-side builder of one RT launch (SynBatchRt, ec_internal.hpp): objects
+// whose survivors are outside the syndrome kernel's points, each with its own
+// coefficient rows.  Any two objects may share a tile (the kernel reads each
+// half's own rows); the tile's row count is the larger of its halves', so
+// halves are paired in order of row count.  One pinned slot holds the
+// objects, the tiles and -- device side only, written by the coefficient
+// kernel -- the rows.  fill() may run on several threads for distinct i.
+struct RtBatchBuild {
+  uint32_t k, n;
+  ParamSlot *slot = nullptr;
+  size_t cap_tiles = 0, o_tiles = 0, o_coef = 0;
+  uint64_t cap_rows = 0;
+  SynBatchObj *objs = nullptr;
+  uint32_t nobj = 0;
+  std::vector<uint32_t> obj_halves;
+
+  static size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
+
+  hipError_t begin(uint32_t count, uint64_t halves, uint64_t rows) {
+    nobj = count;
+    cap_tiles = (size_t)(halves + 1) / 2 + 1;
+    cap_rows = rows;
+    o_tiles = up16(((size_t)count + 1) * sizeof(SynBatchObj));
+    o_coef = up16(o_tiles + cap_tiles * sizeof(SynBatchTile));
+    hipError_t e = param_acquire(o_coef + cap_rows * k * sizeof(uint16_t) + 16, &slot);
+    if (e == hipSuccess) objs = reinterpret_cast<SynBatchObj *>(slot->h);
+    obj_halves.assign(count, 0);
+    return e;
+  }
+  // Descriptor i of survivors nd (chunks ch; ids < 256), rows at the points
+  // rowp[0..ne) stored from row `row0` of the slot's coefficient area: slot a
+  // < k holds point a if it survives, else the next survivor beyond k - 1.
+  SynBatchObj &fill(uint32_t i, const uint16_t *nd, const uint8_t *const *ch, const uint8_t *rowp, uint32_t ne,
+                    uint64_t row0, uint32_t halves) {
+    SynBatchObj &d = objs[i];
+    int at[kMaxFastK];
+    for (uint32_t a = 0; a < k; ++a) at[a] = -1;
+    uint32_t extra[kMaxFastK], nx = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+      if (nd[j] < k)
+        at[nd[j]] = (int)j;
+      else
+        extra[nx++] = j;
+    }
+    uint64_t borrowed = 0;
+    for (uint32_t a = 0, x = 0; a < k; ++a) {
+      uint32_t j;
+      if (at[a] >= 0) {
+        j = (uint32_t)at[a];
+      } else {
+        j = extra[x++];
+        borrowed |= 1ull << a;
+      }
+      d.chunks[a] = ch[j];
+      d.rt.spoint[a] = (uint8_t)nd[j];
+      if (j == 0) d.first = a;
+    }
+    d.rt.borrowed = borrowed;
+    d.rt.ne = ne;
+    for (uint32_t m = 0; m < ne; ++m) d.rt.epoint[m] = rowp[m];
+    d.rt.coef = reinterpret_cast<const uint16_t *>(slot->d + o_coef + row0 * k * sizeof(uint16_t));
+    d.plan = 0;
+    obj_halves[i] = halves;
+    return d;
+  }
+  int launch(bool regen, hipStream_t s) {
+    if (nobj == 0) return hip_status(param_release(slot, s));
+    const uint32_t empty = nobj;
+    std::memset(&objs[empty], 0, sizeof(SynBatchObj));
+    // objects by row count (counting sort), halves paired in that order
+    std::vector<uint32_t> cnt(kMaxFastK + 2, 0), order(nobj);
+    for (uint32_t o = 0; o < nobj; ++o) ++cnt[objs[o].rt.ne + 1];
+    for (uint32_t r = 1; r < cnt.size(); ++r) cnt[r] += cnt[r - 1];
+    for (uint32_t o = 0; o < nobj; ++o) order[cnt[objs[o].rt.ne]++] = o;
+    uint64_t total = 0;
+    for (uint32_t o = 0; o < nobj; ++o) total += obj_halves[o];
+    const uint64_t ntiles = (total + 1) / 2;
+    if (ntiles > cap_tiles || ntiles > 0xFFFFFFFFull) {
+      (void)param_release(slot, s);
+      return VDS_EC_EINVAL;
+    }
+    SynBatchTile *tiles = reinterpret_cast<SynBatchTile *>(slot->h + o_tiles);
+    uint64_t i = 0;
+    for (const uint32_t o : order)
+      for (uint32_t h = 0; h < obj_halves[o]; ++h, ++i) {
+        SynBatchTile &t = tiles[i / 2];
+        if ((i & 1) == 0) t = SynBatchTile{{empty, empty}, {0, 0}, 0, 0, 0, 0};
+        t.obj[i & 1] = o;
+        t.stripe0[i & 1] = h * kHalfStripes;
+        t.nm = std::max(t.nm, objs[o].rt.ne);
+        if (regen && h + 1 == obj_halves[o]) t.trailer |= 1u << (i & 1);
+      }
+    hipError_t e = param_commit(slot, o_tiles + ntiles * sizeof(SynBatchTile), s);
+    const SynBatchObj *dobjs = reinterpret_cast<const SynBatchObj *>(slot->d);
+    if (e == hipSuccess) e = launch_rt_coefs(k, dobjs, nobj, s);
+    if (e == hipSuccess) {
+      SynRestoreArgs sa{};
+      sa.objs = dobjs;
+      sa.tiles = reinterpret_cast<const SynBatchTile *>(slot->d + o_tiles);
+      sa.total_tiles = (uint32_t)ntiles;
+      e = launch_restore_rt_batch(k, n, sa, s, regen);
+    }
+    if (e == hipSuccess && regen) e = launch_regen_tail_rt(k, dobjs, nobj, s);
+    const hipError_t re = param_release(slot, s);
+    if (e == hipSuccess) e = re;
+    return hip_status(e);
+  }
+  void abandon(hipStream_t s) {
+    if (slot) (void)param_release(slot, s);
+  }
+};
+
+// Prefix indices of the routed objects: syn[o] / rt[o] = descriptor index,
+// rtrow[o] = first coefficient row; counts and half / row totals.
+struct BatchIndex {
+  std::vector<uint32_t> syn, rt;
+  std::vector<uint64_t> rtrow;
+  uint32_t nsyn = 0, nrt = 0;
+  uint64_t syn_halves = 0, rt_halves = 0, rt_rows = 0;
+  void build(const std::vector<BatchObjInfo> &info) {
+    const uint32_t count = (uint32_t)info.size();
+    syn.assign(count, 0);
+    rt.assign(count, 0);
+    rtrow.assign(count, 0);
+    for (uint32_t o = 0; o < count; ++o) {
+      const BatchObjInfo &f = info[o];
+      if (f.route == kRouteSyn) {
+        syn[o] = nsyn++;
+        syn_halves += f.halves;
+      } else if (f.route == kRouteRt) {
+        rt[o] = nrt;
+        rtrow[o] = rt_rows;
+        nrt += f.parts;
+        rt_halves += (uint64_t)f.parts * f.halves;
+        rt_rows += f.rows;
+      }
+    }
+  }
+};
+
+// Resolve the syndrome objects' plans (serial: the plan store and the
+// per-call hash), acquire both builders' slots.
+int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, SynBatchBuild &bb, RtBatchBuild &rb,
+                std::vector<uint32_t> &plan, hipStream_t s) {
+  if (ix.nsyn) {
+    hipError_t e = bb.begin(ix.nsyn, ix.syn_halves);
+    if (e != hipSuccess) return hip_status(e);
+    plan.assign(info.size(), 0);
+    for (uint32_t o = 0; o < info.size(); ++o)
+      if (info[o].route == kRouteSyn && (plan[o] = bb.plan_of(info[o].seen)) == UINT32_MAX) {
+        bb.abandon(s);
+        return VDS_EC_ESINGULAR;
+      }
+  }
+  if (ix.nrt) {
+    hipError_t e = rb.begin(ix.nrt, ix.rt_halves, ix.rt_rows);
+    if (e != hipSuccess) {
+      if (ix.nsyn) bb.abandon(s);
+      return hip_status(e);
+    }
+  }
+  return VDS_EC_OK;
+}
+
+int batch_launch(const BatchIndex &ix, SynBatchBuild &bb, RtBatchBuild &rb, bool regen, hipStream_t s) {
+  int rc = ix.nsyn ? bb.launch(regen, s) : VDS_EC_OK;
+  if (rc) {
+    if (ix.nrt) rb.abandon(s);
+    return rc;
+  }
+  return ix.nrt ? rb.launch(regen, s) : VDS_EC_OK;
+}
+
 int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
                          const uint64_t *chunk_sizes, const uint16_t *paddings, uint8_t *const *outs, unsigned flags,
                          hipStream_t s) {
   if (k == 0 || (count && (!nodes || !chunks || !chunk_sizes || !paddings || !outs))) return VDS_EC_EINVAL;
   if (count == 0) return VDS_EC_OK;
-  // every object is validated before anything is enqueued
+  const uint32_t n = k + k / 4;
+  const bool batch_ok = !(flags & VDS_EC_F_CELLS) && k % 4 == 0 && has_restore_syn(k, n);
+  const bool syn = batch_ok && !restore_path_override_bs();
+  // pass 1 (parallel): every object validated before anything is enqueued,
+  // its route and sizes
   std::vector<uint64_t> lens(count);
-  uint64_t halves = 0;
-  for (uint32_t o = 0; o < count; ++o) {
-    int rc = check_restore_args(k, nodes + (uint64_t)o * k, chunks + (uint64_t)o * k, chunk_sizes[o]);
-    if (rc) return rc;
-    bool ok = true;
-    lens[o] = restored_len(2, k, chunk_sizes[o], paddings[o], flags, &ok);
-    if (!ok) return VDS_EC_ERESTORE;
-    if (lens[o] && !outs[o]) return VDS_EC_EINVAL;
-    if (lens[o] && !ids_distinct(k, nodes + (uint64_t)o * k)) return VDS_EC_ESINGULAR;
-    const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);  // stripes that produce output
-    halves += (need + kHalfStripes - 1) / kHalfStripes;
-  }
+  std::vector<BatchObjInfo> info(count);
+  FirstError err;
+  parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
+    for (uint32_t o = o0; o < o1; ++o) {
+      const uint16_t *nd = nodes + (uint64_t)o * k;
+      int rc = check_restore_args(k, nd, chunks + (uint64_t)o * k, chunk_sizes[o]);
+      bool ok = true;
+      if (!rc) lens[o] = restored_len(2, k, chunk_sizes[o], paddings[o], flags, &ok);
+      if (!rc && !ok) rc = VDS_EC_ERESTORE;
+      if (!rc && lens[o] && !outs[o]) rc = VDS_EC_EINVAL;
+      BatchObjInfo f{};
+      uint32_t maxid = 0;
+      if (!rc && lens[o] && !id_set(k, nd, &f.seen, &maxid)) rc = VDS_EC_ESINGULAR;
+      if (rc) {
+        err.note(o, rc);
+        return;
+      }
+      const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);  // stripes that produce output
+      f.halves = (uint32_t)std::min<uint64_t>((need + kHalfStripes - 1) / kHalfStripes, UINT32_MAX);
+      // (SynBatchTile::stripe0 is 32-bit: objects past 2^32 stripes take the per-object path)
+      const bool fits = need <= 0xFFFFFFFFull - kHalfStripes;
+      if (need == 0) {
+        f.route = kRouteSkip;
+      } else if (syn && fits && maxid < n) {
+        f.route = kRouteSyn;
+      } else if (batch_ok && fits && maxid < 256) {
+        f.route = kRouteRt;
+        f.parts = 1;
+        f.rows = (uint16_t)(k - __builtin_popcountll(f.seen & ((1ull << k) - 1)));  // erased points below k
+      } else {
+        f.route = kRouteOne;
+      }
+      info[o] = f;
+    }
+  });
+  if (err.rc) return err.rc;
   int rc = device_ready();
   if (rc) return rc;
-  const uint32_t n = k + k / 4;
-  const bool syn = !(flags & VDS_EC_F_CELLS) && k % 4 == 0 && has_restore_syn(k, n) && !restore_path_override_bs();
-  std::vector<uint32_t> fallback;
+  BatchIndex ix;
+  ix.build(info);
   SynBatchBuild bb{k, n};
-  if (syn) {
-    hipError_t e = bb.begin(count, halves);
-    if (e != hipSuccess) return hip_status(e);
-  }
-  uint8_t pos[64];
+  RtBatchBuild rb{k, n};
+  std::vector<uint32_t> plan;
+  if ((rc = batch_begin(info, ix, bb, rb, plan, s))) return rc;
+  // pass 2 (parallel): the descriptors
+  parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
+    for (uint32_t o = o0; o < o1; ++o) {
+      const BatchObjInfo &f = info[o];
+      const uint16_t *nd = nodes + (uint64_t)o * k;
+      const uint8_t *const *ch = chunks + (uint64_t)o * k;
+      SynBatchObj *d;
+      if (f.route == kRouteSyn) {
+        d = &bb.fill(ix.syn[o], f.seen, nd, ch, plan[o], f.halves);
+      } else if (f.route == kRouteRt) {
+        uint8_t rowp[kMaxFastK];
+        uint32_t ne = 0;
+        for (uint64_t b = ~f.seen & ((1ull << k) - 1); b; b &= b - 1) rowp[ne++] = (uint8_t)__builtin_ctzll(b);
+        d = &rb.fill(ix.rt[o], nd, ch, rowp, ne, ix.rtrow[o], f.halves);
+      } else {
+        continue;
+      }
+      d->out = outs[o];
+      std::memset(d->regen, 0, sizeof d->regen);
+      d->out_len = lens[o];
+      d->chunk_len = chunk_sizes[o];
+    }
+  });
+  if ((rc = batch_launch(ix, bb, rb, false, s))) return rc;
   for (uint32_t o = 0; o < count; ++o) {
-    uint64_t seen = 0;
-    const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);
-    // (SynBatchTile::stripe0 is 32-bit: objects past 2^32 stripes take the
-    // per-object path)
-    if (!syn || need > 0xFFFFFFFFull - kHalfStripes || !syn_survivors(k, n, nodes + (uint64_t)o * k, &seen, pos)) {
-      fallback.push_back(o);
-      continue;
-    }
-    if (need == 0) continue;
-    const uint64_t h = (need + kHalfStripes - 1) / kHalfStripes;
-    SynBatchObj *d = bb.add(seen, chunks + (uint64_t)o * k, pos, h);
-    if (!d) {
-      bb.abandon(s);
-      return VDS_EC_ESINGULAR;
-    }
-    d->out = outs[o];
-    std::memset(d->regen, 0, sizeof d->regen);
-    d->out_len = lens[o];
-    d->chunk_len = chunk_sizes[o];
-  }
-  if (syn && (rc = bb.launch(false, s))) return rc;
-  for (uint32_t o : fallback) {
-    if (lens[o] == 0) continue;
+    if (info[o].route != kRouteOne) continue;
     std::vector<uint16_t> m((size_t)k * k);
     rc = inverse16(k, nodes + (uint64_t)o * k, m.data());
     if (rc) return rc;
@@ -1252,59 +1582,105 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
                             hipStream_t s) {
   if (k == 0 || (count && (!nodes || !chunks || !chunk_sizes || (nt && (!targets || !outs))))) return VDS_EC_EINVAL;
   if (count == 0 || nt == 0) return VDS_EC_OK;
-  uint64_t halves = 0;
-  for (uint32_t o = 0; o < count; ++o) {
-    if (chunk_sizes[o] < 2 || (chunk_sizes[o] - 2) % 2) return VDS_EC_EINVAL;  // cells + BE16 trailer
-    for (uint32_t j = 0; j < k; ++j)
-      if (!chunks[(uint64_t)o * k + j]) return VDS_EC_EINVAL;
-    for (uint32_t i = 0; i < nt; ++i)
-      if (!outs[(uint64_t)o * nt + i]) return VDS_EC_EINVAL;
-    if (!ids_distinct(k, nodes + (uint64_t)o * k)) return VDS_EC_ESINGULAR;
-    const uint64_t T = (chunk_sizes[o] - 2) / 2;
-    halves += T ? (T + kHalfStripes - 1) / kHalfStripes : 1;
-  }
+  // Routes as restore_batch_device's; the syndrome kernel only when every
+  // target is one of the object's erased points (each at most once: wave w
+  // recovers the w-th erased point, ascending); an RT object carries at most
+  // n - k rows, so one with more targets becomes several descriptors, each
+  // re-reading its survivors.
+  const uint32_t n = k + k / 4, R = n - k;
+  const bool batch_ok = k % 4 == 0 && has_restore_syn(k, n);
+  const bool syn = batch_ok && !restore_path_override_bs();
+  std::vector<BatchObjInfo> info(count);
+  FirstError err;
+  parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
+    for (uint32_t o = o0; o < o1; ++o) {
+      const uint16_t *nd = nodes + (uint64_t)o * k;
+      const uint16_t *tg = targets + (uint64_t)o * nt;
+      int rc = VDS_EC_OK;
+      if (chunk_sizes[o] < 2 || (chunk_sizes[o] - 2) % 2) rc = VDS_EC_EINVAL;  // cells + BE16 trailer
+      for (uint32_t j = 0; !rc && j < k; ++j)
+        if (!chunks[(uint64_t)o * k + j]) rc = VDS_EC_EINVAL;
+      for (uint32_t i = 0; !rc && i < nt; ++i)
+        if (!outs[(uint64_t)o * nt + i]) rc = VDS_EC_EINVAL;
+      BatchObjInfo f{};
+      uint32_t maxid = 0;
+      if (!rc && !id_set(k, nd, &f.seen, &maxid)) rc = VDS_EC_ESINGULAR;
+      if (rc) {
+        err.note(o, rc);
+        return;
+      }
+      const uint64_t T = (chunk_sizes[o] - 2) / 2;
+      f.halves = (uint32_t)std::min<uint64_t>(T ? (T + kHalfStripes - 1) / kHalfStripes : 1, UINT32_MAX);
+      const bool fits = T <= 0xFFFFFFFFull - kHalfStripes;
+      bool ok = syn && fits && maxid < n;
+      const uint64_t erased = ~f.seen & ((1ull << n) - 1);
+      uint64_t hit = 0;
+      uint32_t tmax = 0;
+      for (uint32_t i = 0; i < nt; ++i) {
+        const uint32_t t = tg[i];
+        tmax = t > tmax ? t : tmax;
+        if (ok) {
+          ok = t < n && ((erased >> t) & 1u) && !((hit >> t) & 1u);
+          if (ok) hit |= 1ull << t;
+        }
+      }
+      if (ok) {
+        f.route = kRouteSyn;
+      } else if (batch_ok && fits && maxid < 256 && tmax < 256) {
+        f.route = kRouteRt;
+        f.parts = (uint8_t)((nt + R - 1) / R);
+        f.rows = (uint16_t)nt;
+      } else {
+        f.route = kRouteOne;
+      }
+      info[o] = f;
+    }
+  });
+  if (err.rc) return err.rc;
   int rc = device_ready();
   if (rc) return rc;
-  const uint32_t n = k + k / 4;
-  const bool syn = k % 4 == 0 && has_restore_syn(k, n) && !restore_path_override_bs();
-  std::vector<uint32_t> fallback;
+  for (const BatchObjInfo &f : info)  // (RT descriptors per object: nt / (n - k) rounded up, < 256)
+    if (f.route == kRouteRt && (uint32_t)f.parts * R < nt) return VDS_EC_EINVAL;
+  BatchIndex ix;
+  ix.build(info);
   SynBatchBuild bb{k, n};
-  if (syn) {
-    hipError_t e = bb.begin(count, halves);
-    if (e != hipSuccess) return hip_status(e);
-  }
-  uint8_t pos[64];
+  RtBatchBuild rb{k, n};
+  std::vector<uint32_t> plan;
+  if ((rc = batch_begin(info, ix, bb, rb, plan, s))) return rc;
+  parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
+    for (uint32_t o = o0; o < o1; ++o) {
+      const BatchObjInfo &f = info[o];
+      const uint16_t *nd = nodes + (uint64_t)o * k;
+      const uint8_t *const *ch = chunks + (uint64_t)o * k;
+      const uint16_t *tg = targets + (uint64_t)o * nt;
+      uint8_t *const *os = outs + (uint64_t)o * nt;
+      if (f.route == kRouteSyn) {
+        SynBatchObj &d = bb.fill(ix.syn[o], f.seen, nd, ch, plan[o], f.halves);
+        const uint64_t erased = ~f.seen & ((1ull << n) - 1);
+        std::memset(d.regen, 0, sizeof d.regen);
+        for (uint32_t i = 0; i < nt; ++i)
+          d.regen[__builtin_popcountll(erased & ((1ull << tg[i]) - 1))] = os[i];
+        d.out = nullptr;
+        d.out_len = 0;
+        d.chunk_len = chunk_sizes[o];
+      } else if (f.route == kRouteRt) {
+        for (uint32_t part = 0, i0 = 0; part < f.parts; ++part, i0 += R) {
+          const uint32_t cnt = std::min(R, nt - i0);
+          uint8_t rowp[kMaxFastK / 4];
+          for (uint32_t i = 0; i < cnt; ++i) rowp[i] = (uint8_t)tg[i0 + i];
+          SynBatchObj &d = rb.fill(ix.rt[o] + part, nd, ch, rowp, cnt, ix.rtrow[o] + i0, f.halves);
+          std::memset(d.regen, 0, sizeof d.regen);
+          for (uint32_t i = 0; i < cnt; ++i) d.regen[i] = os[i0 + i];
+          d.out = nullptr;
+          d.out_len = 0;
+          d.chunk_len = chunk_sizes[o];
+        }
+      }
+    }
+  });
+  if ((rc = batch_launch(ix, bb, rb, true, s))) return rc;
   for (uint32_t o = 0; o < count; ++o) {
-    uint64_t seen = 0;
-    const uint64_t T = (chunk_sizes[o] - 2) / 2;
-    bool ok = syn && T <= 0xFFFFFFFFull - kHalfStripes && syn_survivors(k, n, nodes + (uint64_t)o * k, &seen, pos);
-    // every target must be an erased point, each at most once: wave w
-    // recovers the w-th erased point (ascending)
-    uint8_t *regen[kMaxFastK / 4] = {};
-    const uint64_t erased = ~seen & ((1ull << n) - 1);
-    for (uint32_t i = 0; ok && i < nt; ++i) {
-      const uint32_t t = targets[(uint64_t)o * nt + i];
-      const uint32_t w = t < n ? (uint32_t)__builtin_popcountll(erased & ((1ull << t) - 1)) : 0;
-      ok = t < n && ((erased >> t) & 1u) && !regen[w];
-      if (ok) regen[w] = outs[(uint64_t)o * nt + i];
-    }
-    if (!ok) {
-      fallback.push_back(o);
-      continue;
-    }
-    const uint64_t h = T ? (T + kHalfStripes - 1) / kHalfStripes : 1;
-    SynBatchObj *d = bb.add(seen, chunks + (uint64_t)o * k, pos, h);
-    if (!d) {
-      bb.abandon(s);
-      return VDS_EC_ESINGULAR;
-    }
-    d->out = nullptr;
-    std::memcpy(d->regen, regen, sizeof regen);
-    d->out_len = 0;
-    d->chunk_len = chunk_sizes[o];
-  }
-  if (syn && (rc = bb.launch(true, s))) return rc;
-  for (uint32_t o : fallback) {
+    if (info[o].route != kRouteOne) continue;
     rc = regenerate_device(2, k, nodes + (uint64_t)o * k, chunks + (uint64_t)o * k, chunk_sizes[o], 0, 1,
                            targets + (uint64_t)o * nt, nt, outs + (uint64_t)o * nt, 0, s);
     if (rc) return rc;

@@ -36,6 +36,11 @@ int main() {
   CHECK(gf8_mul(0x53, 0xCA) == 0x8F);
   CHECK(gf8_mul(2, 0x80) == 0x1D);
   for (int t = 0; t < 1000; ++t) { uint32_t a = rnd() & 0xFFFF; if (a) CHECK(gf16_mul(a, gf16_inv(a)) == 1); }
+  // the RT coefficient kernel's Itoh-Tsujii inverse and linear squaring, every element
+  for (uint32_t a = 0; a < 65536; ++a) {
+    CHECK(gf16_inv_it(a) == gf16_inv(a));
+    CHECK(gf16_sqr(a) == gf16_mul(a, a));
+  }
   // transpose32
   uint32_t A[32], B[32];
   for (int i = 0; i < 32; ++i) A[i] = B[i] = rnd();

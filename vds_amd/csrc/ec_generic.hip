@@ -266,35 +266,41 @@ __global__ void k_regen_tail_batch(uint32_t k, uint32_t m, const SynBatchObj *ob
 //   l_j(t) = prod_{i != j} (t + a_i) / D_j,  D_j = prod_{i != j} (a_j + a_i),
 // the numerator an exclusive product across the lanes (prefix x suffix
 // scans), so the only inversion is D_j's, once per slot.  t equal to a slot's
-// point gives the unit row, as it must.
+// point gives the unit row, as it must.  k <= 32: the wave's two halves take
+// two rows at a time (32-lane scans).
 __global__ void k_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count) {
   const int lane = threadIdx.x & 63;
+  const int seg = k <= 32 ? 32 : 64;  // lanes per row
+  const int j = lane & (seg - 1);     // slot of this lane
+  const int half = lane / seg;        // row of this lane within a pass
+  const uint32_t per_pass = 64 / seg;
   const uint32_t waves = blockDim.x / 64;
   for (uint32_t o = blockIdx.x * waves + (threadIdx.x >> 6); o < count; o += gridDim.x * waves) {
     const SynBatchRt &r = objs[o].rt;
     const uint32_t ne = r.ne;
     if (ne == 0) continue;
-    const bool live = lane < (int)k;
-    const uint32_t a = live ? r.spoint[lane] : 0u;
-    uint32_t D = 1;
-    for (uint32_t j = 0; j < k; ++j) {
-      const uint32_t aj = __shfl(a, (int)j);
-      D = gf16_mul(D, j == (uint32_t)lane ? 1u : (a ^ aj));
+    const bool live = j < (int)k;
+    const uint32_t a = live ? r.spoint[j] : 0u;
+    // D_j in four independent chains (ILP)
+    uint32_t d4[4] = {1u, 1u, 1u, 1u};
+    for (uint32_t i = 0; i < k; ++i) {
+      const uint32_t ai = __shfl(a, (int)i);
+      d4[i & 3] = gf16_mul(d4[i & 3], i == (uint32_t)j ? 1u : (a ^ ai));
     }
-    const uint32_t invD = gf16_inv(D);
+    const uint32_t invD = gf16_inv_it(gf16_mul(gf16_mul(d4[0], d4[1]), gf16_mul(d4[2], d4[3])));
     uint16_t *const out = const_cast<uint16_t *>(r.coef);
-    for (uint32_t m = 0; m < ne; ++m) {
-      const uint32_t f = live ? (r.epoint[m] ^ a) : 1u;
-      uint32_t pre = f, suf = f;  // inclusive prefix / suffix products over the lanes
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
+    for (uint32_t m0 = 0; m0 < ne; m0 += per_pass) {
+      const uint32_t m = m0 + (uint32_t)half;
+      const uint32_t f = live && m < ne ? (r.epoint[m] ^ a) : 1u;
+      uint32_t pre = f, suf = f;  // inclusive prefix / suffix products within the row's lanes
+      for (int off = 1; off < seg; off <<= 1) {
         const uint32_t u = __shfl_up(pre, off), w = __shfl_down(suf, off);
-        if (lane >= off) pre = gf16_mul(pre, u);
-        if (lane + off < 64) suf = gf16_mul(suf, w);
+        if (j >= off) pre = gf16_mul(pre, u);
+        if (j + off < seg) suf = gf16_mul(suf, w);
       }
       const uint32_t before = __shfl_up(pre, 1), after = __shfl_down(suf, 1);
-      const uint32_t excl = gf16_mul(lane == 0 ? 1u : before, lane == 63 ? 1u : after);
-      if (live) out[(uint64_t)m * k + lane] = (uint16_t)gf16_mul(excl, invD);
+      const uint32_t excl = gf16_mul(j == 0 ? 1u : before, j == seg - 1 ? 1u : after);
+      if (live && m < ne) out[(uint64_t)m * k + j] = (uint16_t)gf16_mul(excl, invD);
     }
   }
 }

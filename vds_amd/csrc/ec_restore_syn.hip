@@ -275,8 +275,10 @@ __device__ __forceinline__ void rec_pair(Plane16 &acc, const Plane16 &t, const P
 // ones -- and acc ^= (T & ma) ^ (T1 & mb) is one masked v_bitop3 per plane
 // and nonzero mask.  (Seven specialised arms per bit pair, as rec_pair's,
 // made the unrolled walk ~128 KiB of code: it thrashed the instruction cache,
-// 4x slower per tile.)  The mask is copied to a VGPR first: a v_bitop3
-// reading an SGPR issues at ~0.6 of the all-VGPR rate.
+// 4x slower per tile; one arm per mask value, with the masks preloaded in
+// VGPRs, measured no faster than this copy of the mask: 363 vs 377 GiB/s.)
+// The mask is copied to a VGPR first: a v_bitop3 reading an SGPR issues at
+// ~0.6 of the all-VGPR rate.
 constexpr uint32_t kRtH0 = 0x00FF00FFu, kRtH1 = 0xFF00FF00u;
 #define VDS_RD_MA(i) "v_bitop3_b32 %[c" #i "], %[c" #i "], %[a" #i "], %[tm] bitop3:0x78\n"
 #define VDS_RD_MB(i) "v_bitop3_b32 %[c" #i "], %[c" #i "], %[b" #i "], %[tm] bitop3:0x78\n"
@@ -305,12 +307,6 @@ __device__ __forceinline__ void rec_dual(Plane16 &acc, const Plane16 &t, const P
 #undef VDS_RS_XA
 #undef VDS_RS_XB
 #undef VDS_RS_X3
-
-// Coefficient idx of a wave-uniform uint16 table (s_load of its dword).
-__device__ __forceinline__ uint32_t s_ld_u16(const uint16_t *arr, uint32_t idx) {
-  const uint32_t w = s_ld(reinterpret_cast<const uint32_t *>(arr) + (idx >> 1));
-  return (w >> (16 * (idx & 1))) & 0xFFFFu;
-}
 
 // LDS XOR of a point's sixteen planes (this lane's 64 bytes) as eight
 // ds_xor_b64: planes 4g..4g+3 of point pt at byte (4 pt + g) 1 KiB + 16 lane.
@@ -565,19 +561,32 @@ void k_restore_syn(SynRestoreArgs a) {
         Plane16 ce[kMC];
 #pragma unroll
         for (int m = 0; m < kMC; ++m) ce[m] = plane_zero();
+        // this wave's kLoadPer = 4 slot coefficients of each row, both
+        // halves: 8 contiguous bytes per (half, row), all issued at once
+        static_assert(S::kLoadPer == 4, "one 8-byte scalar load per row and half");
+        uint64_t q0[kMC], q1[kMC];
+#pragma unroll
+        for (int m = 0; m < kMC; ++m) {
+          const uint32_t at = (m0 + m) * K + wave * S::kLoadPer;
+          q0[m] = m0 + m < ne0 ? s_ld(reinterpret_cast<const uint64_t *>(cf0 + at)) : 0ull;
+          q1[m] = m0 + m < ne1 ? s_ld(reinterpret_cast<const uint64_t *>(cf1 + at)) : 0ull;
+        }
 #pragma unroll
         for (int s = 0; s < S::kLoadPer; ++s) {
-          const uint32_t j = wave * S::kLoadPer + s;
           uint32_t c0[kMC], c1[kMC];
 #pragma unroll
           for (int m = 0; m < kMC; ++m) {
-            c0[m] = m0 + m < ne0 ? s_ld_u16(cf0, (m0 + m) * K + j) : 0u;
-            c1[m] = m0 + m < ne1 ? s_ld_u16(cf1, (m0 + m) * K + j) : 0u;
+            c0[m] = (uint32_t)(q0[m] >> (16 * s)) & 0xFFFFu;
+            c1[m] = (uint32_t)(q1[m] >> (16 * s)) & 0xFFFFu;
           }
           // (one slot's chain at a time: interleaving the four independent
           // chains would not fit beside the accumulators)
           __builtin_amdgcn_sched_barrier(0);
           Plane16 tt = Ps[s];
+          // (opaque per row pair: the chains do not depend on m0, and hoisted
+          // out of the loop all 4 x 16 of them spilled)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(tt.p[i]));
 #pragma unroll
           for (int b = 0; b < 16; b += 2) {
             __builtin_amdgcn_sched_barrier(0);

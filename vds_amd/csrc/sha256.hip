@@ -72,6 +72,12 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[
 }
 
 // Message j = base + j * stride (len bytes) -> digest at digests + 32 j.
+// ALIGNED (base and stride multiples of 16, e.g. the replica layouts of the
+// batched encodes): whole blocks as four 16-byte loads per lane, the next
+// block's loads issued before this block's 64 rounds (each lane walks its
+// own message: without the prefetch every block waited out a full memory
+// latency).  Otherwise aligned dwords and one v_perm_b32 per word.
+template <bool ALIGNED>
 __global__ __launch_bounds__(64) void k_sha256(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count,
                                                uint8_t *digests) {
   const uint32_t j = blockIdx.x * 64u + threadIdx.x;
@@ -83,24 +89,48 @@ __global__ __launch_bounds__(64) void k_sha256(const uint8_t *base, uint64_t len
 
   // Whole blocks from aligned dwords: block b needs dwords 16 b .. 16 b + 16
   // of p (17 with the misalignment), all inside the message while
-  // 64 b + 68 <= len + sh.
-  const uint32_t sh = (uint32_t)((uintptr_t)m & 3u);
+  // 64 b + 68 <= len + sh.  (ALIGNED: sh = 0 and 64 b + 64 <= len.)
+  const uint32_t sh = ALIGNED ? 0u : (uint32_t)((uintptr_t)m & 3u);
   const uint32_t *p = reinterpret_cast<const uint32_t *>(m - sh);
   // big-endian word of message bytes 4i..4i+3 = bytes sh+3, sh+2, sh+1, sh of (p[i+1]:p[i])
   const uint32_t sel = (sh + 3u) | ((sh + 2u) << 8) | ((sh + 1u) << 16) | (sh << 24);
-  const uint64_t nfast = len + sh >= 68 ? (len + sh - 68) / 64 + 1 : 0;
-  uint32_t carry = nfast ? p[0] : 0u;
-  for (uint64_t blk = 0; blk < nfast; ++blk) {
-    const uint32_t *q = p + 16 * blk;
-    uint32_t raw[17];
-    raw[0] = carry;
+  uint64_t nfast;
+  if constexpr (ALIGNED) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(m);
+    nfast = len / 64;
+    u32x4 nx[4];
+    if (nfast) {
 #pragma unroll
-    for (int i = 1; i <= 16; ++i) raw[i] = q[i];
-    carry = raw[16];
-    uint32_t w[16];
+      for (int i = 0; i < 4; ++i) nx[i] = q[i];
+    }
+    for (uint64_t blk = 0; blk < nfast; ++blk) {
+      uint32_t w[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(raw[i + 1], raw[i], sel);
-    sha256_compress(h, w);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) w[4 * i + t] = __builtin_amdgcn_perm(0u, nx[i][t], 0x00010203u);
+      if (blk + 1 < nfast) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) nx[i] = q[4 * (blk + 1) + i];
+      }
+      sha256_compress(h, w);
+    }
+  } else {
+    nfast = len + sh >= 68 ? (len + sh - 68) / 64 + 1 : 0;
+    uint32_t carry = nfast ? p[0] : 0u;
+    for (uint64_t blk = 0; blk < nfast; ++blk) {
+      const uint32_t *q = p + 16 * blk;
+      uint32_t raw[17];
+      raw[0] = carry;
+#pragma unroll
+      for (int i = 1; i <= 16; ++i) raw[i] = q[i];
+      carry = raw[16];
+      uint32_t w[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(raw[i + 1], raw[i], sel);
+      sha256_compress(h, w);
+    }
   }
 
   // The rest (< 132 bytes) the same way, from the aligned dwords that hold at
@@ -143,7 +173,10 @@ __global__ __launch_bounds__(64) void k_sha256(const uint8_t *base, uint64_t len
 hipError_t launch_sha256(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count, uint8_t *digests,
                          hipStream_t s) {
   if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sha256, dim3((count + 63) / 64), dim3(64), 0, s, base, len, stride, count, digests);
+  if ((((uintptr_t)base | stride) & 15u) == 0)
+    hipLaunchKernelGGL(k_sha256<true>, dim3((count + 63) / 64), dim3(64), 0, s, base, len, stride, count, digests);
+  else
+    hipLaunchKernelGGL(k_sha256<false>, dim3((count + 63) / 64), dim3(64), 0, s, base, len, stride, count, digests);
   return hipGetLastError();
 }
 

@@ -34,7 +34,7 @@ def _first_k_found(rng, k, n_total, lost):
     return [r for r in range(n_total) if r not in gone][:k]
 
 
-@pytest.mark.parametrize("k,n_total", [(16, 20), (32, 40), (32, 64)])
+@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 40), (32, 40), (32, 64)])
 def test_restore_batch_per_object_survivors(gpu, k, n_total):
     import torch
     from vds_amd import chunk
@@ -64,7 +64,7 @@ def test_restore_batch_per_object_survivors(gpu, k, n_total):
         assert (got[size:] == 0xA5).all(), size  # nothing written past the object
 
 
-@pytest.mark.parametrize("k,n_total", [(16, 20), (32, 40), (32, 64)])
+@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 40), (32, 40), (32, 64)])
 def test_regenerate_batch_per_object(gpu, k, n_total):
     import torch
     from vds_amd import chunk
@@ -136,3 +136,55 @@ def test_batch_pairs_halves_of_small_objects(gpu, k, n_total):
         g = r.cpu().numpy()
         assert np.array_equal(g[:c], O.encode(k, tg[0], host)), (size, tg)
         assert (g[c:] == 0x5A).all()
+
+
+@pytest.mark.parametrize("k", [16, 32])
+def test_batch_routes_mixed(gpu, k):
+    """One call whose objects take every route: the syndrome batch (survivors
+    within 0..k+k/4-1), the RT batch (any other ids < 256, rows = erased
+    points below k; regenerate: more targets than n - k split into several
+    descriptors), and the per-object path (an id >= 256).  Every object
+    against the oracle."""
+    import torch
+    from vds_amd import chunk
+    rng = np.random.default_rng(900 + k)
+    n = k + k // 4
+    tile = 2048 * 2 * k
+    sizes = [tile // 2, tile + 3 * k, 1000, tile // 2 - 2 * k, 2 * tile + 1, 77, tile // 2, tile]
+    ids_of = [
+        list(range(k)),                                           # syn, nothing erased below k
+        [r for r in range(n) if r not in (1, 2)][:k],             # syn
+        list(range(3, 3 + k)),                                    # RT: survivors up to k + 2 < n? (syn when < n)
+        [0, 300] + list(range(2, k)),                             # per object: id >= 256
+        list(range(k // 2)) + list(range(n, n + k // 2)),         # RT: half the points below k erased
+        list(range(200, 200 + k)),                                # RT: every point below k erased
+        list(rng.permutation(list(range(1, k)) + [n + 5])),       # RT, any order
+        list(range(k - 1)) + [255],                               # RT: id 255
+    ]
+    hosts, reps_of, nodes, chunks, csz, pads, outs = [], [], [], [], [], [], []
+    for size, nd in zip(sizes, ids_of):
+        host = O.splitmix(SEED + 31 * size + k, size)
+        L = chunk.replica_size(k, size)
+        reps = {r: torch.from_numpy(O.encode(k, r, host)).cuda() for r in nd}
+        hosts.append(host)
+        reps_of.append(reps)
+        nodes.append(nd)
+        chunks.append([reps[r].data_ptr() for r in nd])
+        csz.append(L)
+        pads.append(size % (2 * k))
+        outs.append(torch.full((size + 64,), 0xA5, dtype=torch.uint8, device="cuda"))
+    chunk.restore_batch_device(k, nodes, chunks, csz, pads, [o.data_ptr() for o in outs])
+    # regenerate: n - k + 3 targets each (more than one RT descriptor holds)
+    nt = n - k + 3
+    targets = [sorted(rng.choice([r for r in range(260) if r not in nd], nt, replace=False).tolist()) for nd in nodes]
+    rg = [[torch.full((c + 8,), 0x5A, dtype=torch.uint8, device="cuda") for _ in range(nt)] for c in csz]
+    chunk.regenerate_batch_device(k, nodes, chunks, csz, targets, [[x.data_ptr() for x in r] for r in rg])
+    torch.cuda.synchronize()
+    for i, (host, size) in enumerate(zip(hosts, sizes)):
+        got = outs[i].cpu().numpy()
+        assert np.array_equal(got[:size], host), (i, nodes[i])
+        assert (got[size:] == 0xA5).all()
+        for t, x in zip(targets[i], rg[i]):
+            g = x.cpu().numpy()
+            assert np.array_equal(g[:csz[i]], O.encode(k, t, host)), (i, t)
+            assert (g[csz[i]:] == 0x5A).all()

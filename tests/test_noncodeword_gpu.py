@@ -106,7 +106,7 @@ def test_restore_noncodeword_paths(gpu, k, nodes, T, path, pmode):
         assert (got[o, E:] == 0xA5).all(), "wrote past E"
 
 
-@pytest.mark.parametrize("k,n_total", [(16, 20), (32, 40), (32, 64)])
+@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 48), (32, 40), (32, 64)])
 def test_restore_batch_noncodeword(gpu, k, n_total):
     """Batch mode (k_restore_syn BATCH for survivors within its points, the
     per-object fallback for the rest) on random survivors and trailers."""
@@ -184,7 +184,7 @@ def test_regenerate_noncodeword_paths(gpu, k, nodes, targets, T, path, pmode):
             assert (got[i, o, L:] == 0x5A).all()
 
 
-@pytest.mark.parametrize("k,n_total", [(16, 20), (32, 40), (32, 64)])
+@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 48), (32, 40), (32, 64)])
 def test_regenerate_batch_noncodeword(gpu, k, n_total):
     """Batch regenerate (syndrome batch kernel + its device-side tail, and the
     per-object fallback) on random survivors with disagreeing trailers."""

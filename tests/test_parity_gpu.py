@@ -77,6 +77,43 @@ def test_encode_small_golden_host_api(ec):
             assert ec.ChunkGenerator(e["k"], r).write(d).tobytes().hex() == e["replicas"][str(r)]
 
 
+def test_per_replica_loop_window(ec):
+    """The drop-in per-replica loop (save_temp, dht_network_client.cpp:74-79):
+    calls for replicas 0..n-1 of one buffer are served from an encoded window
+    (vds_ec_api.cpp encode_host).  Every call must still give the encode of
+    the buffer's CURRENT bytes: in-place edits, skipped / repeated / backward
+    ids, other shapes in between, and the 8-bit generator."""
+    k, n, size = 32, 64, 65536 - 77
+    d = O.splitmix(SEED + 901, size).copy()
+    gens = [ec.ChunkGenerator(k, r) for r in range(n)]
+    want = {r: O.encode(k, r, d) for r in range(n)}
+    for r in range(n):
+        assert gens[r].write(d).tobytes() == want[r].tobytes(), f"replica {r}"
+    for r in (63, 5, 5, 6, 7, 2, 64, 65):  # out of order, repeated, past the window
+        assert ec.ChunkGenerator(k, r).write(d).tobytes() == O.encode(k, r, d).tobytes(), f"replica {r}"
+    # same buffer edited in place mid-loop: the calls after the edit see it
+    for r in range(10):
+        if r == 4:
+            d[1000] ^= 0x5A
+            want = {q: O.encode(k, q, d) for q in range(4, 10)}
+        got = gens[r].write(d)
+        if r >= 4:
+            assert got.tobytes() == want[r].tobytes(), f"replica {r} after edit"
+    # a different shape / width / trailer flag between calls of the same loop
+    e = O.splitmix(SEED + 902, 4099)
+    assert gens[10].write(d).tobytes() == O.encode(k, 10, d).tobytes()
+    assert ec.ChunkGenerator(16, 11).write(d).tobytes() == O.encode(16, 11, d).tobytes()
+    assert gens[11].write(d, write_padding=False).tobytes() == O.encode(k, 11, d, write_padding=False).tobytes()
+    assert gens[12].write(e).tobytes() == O.encode(k, 12, e).tobytes()
+    assert ec.ChunkGenerator(8, 13, cell_bytes=1).write(e).tobytes() == O.encode(8, 13, e, 1).tobytes()
+    assert ec.ChunkGenerator(8, 14, cell_bytes=1).write(e).tobytes() == O.encode(8, 14, e, 1).tobytes()
+    assert gens[13].write(d).tobytes() == O.encode(k, 13, d).tobytes()
+    # the 8-bit ids stop at 255
+    for r in (253, 254, 255):
+        assert ec.ChunkGenerator(8, r, cell_bytes=1).write(e).tobytes() == O.encode(8, r, e, 1).tobytes()
+    assert ec.chunk.encode_host(k, [3], np.zeros(0, np.uint8))[0].tobytes() == O.encode(k, 3, np.zeros(0, np.uint8)).tobytes()
+
+
 @pytest.mark.parametrize("entry", G["encode16_sha"], ids=lambda e: f"k{e['k']}n{e['n']}s{e['size']}")
 def test_encode_golden_sha(ec, entry):
     import torch

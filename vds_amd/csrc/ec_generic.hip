@@ -305,6 +305,24 @@ __global__ void k_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count) 
   }
 }
 
+// ============================================================ host push copy
+// Device -> host copy by a kernel storing into mapped pinned host memory.
+// On the MI355X box the two SDMA directions together move only one
+// direction's bytes (57 GB/s total: H2D + D2H on two streams at 28.5 each),
+// but a kernel's stores over PCIe run beside an SDMA H2D: 42.7 + 42.7 GB/s
+// (tools/ubench/pcie_duplex.hip).  The host batches therefore take their
+// results out this way while the next group's input comes in by SDMA.
+typedef uint32_t copy_u32x4 __attribute__((ext_vector_type(4)));
+__global__ void k_push(uint8_t *dst, const uint8_t *src, uint64_t bytes) {
+  const uint64_t n16 = bytes / 16;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  for (uint64_t i = i0; i < n16; i += step)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const copy_u32x4 *>(src) + i),
+                                reinterpret_cast<copy_u32x4 *>(dst) + i);
+  for (uint64_t b = 16 * n16 + i0; b < bytes; b += step) dst[b] = src[b];
+}
+
 // ============================================================== synthetic data
 
 __global__ void k_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed) {
@@ -396,6 +414,15 @@ hipError_t launch_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count, 
   if (k > 64) return hipErrorInvalidValue;
   const uint32_t waves = 4, grid = (count + waves - 1) / waves < 8192u ? (count + waves - 1) / waves : 8192u;
   hipLaunchKernelGGL(k_rt_coefs, dim3(grid), dim3(64 * waves), 0, s, k, objs, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_push(uint8_t *dst_host_dev, const uint8_t *src, uint64_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  if (((uintptr_t)dst_host_dev | (uintptr_t)src) & 15u) return hipErrorInvalidValue;
+  uint64_t g = (bytes / 16 + 255) / 256;
+  const uint32_t grid = (uint32_t)(g < 1 ? 1 : (g > 512 ? 512 : g));
+  hipLaunchKernelGGL(k_push, dim3(grid), dim3(256), 0, s, dst_host_dev, src, bytes);
   return hipGetLastError();
 }
 

@@ -254,5 +254,8 @@ bool has_restore_fast(uint32_t k);
 hipError_t launch_sha256(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count, uint8_t *digests,
                          hipStream_t s);
 hipError_t launch_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed, hipStream_t s);
+// Device -> mapped pinned host copy by a kernel (dst: the device view of the
+// host buffer; both 16-byte aligned).
+hipError_t launch_push(uint8_t *dst_host_dev, const uint8_t *src, uint64_t bytes, hipStream_t s);
 
 }  // namespace vds_ec

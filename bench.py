@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-live", action="store_true", help="skip the live-shape line (k=32, n=64, 64 KiB objects)")
     p.add_argument("--no-align16", action="store_true", help="skip the 16-byte replica stride line")
+    p.add_argument("--no-jit", action="store_true",
+                   help="no run-time compiled survivor-set kernel: the repair runs k_restore_syn")
     p.add_argument("--live-objects", type=int, default=16384)
     p.add_argument("--replica-align", type=int, default=256,
                    help="replica buffers start on multiples of this many bytes (1: packed at the odd stride L)")
@@ -149,7 +151,8 @@ def kernel_names(k, n, nodes, size, L, objects):
     ep = _lib.lib().vds_ec_encode16_path(k, ids.ctypes.data_as(_lib.u16p), n, C.c_uint64(size))
     rp = _lib.lib().vds_ec_restore16_path(k, nd.ctypes.data_as(_lib.u16p), C.c_uint64(L), size % (2 * k), objects)
     enc = {2: f"k_encode_bs<{k},{n}>"}.get(ep, "k_encode_generic")
-    rep = {3: f"k_restore_syn<{k},{n}>", 2: f"k_restore_bs<{k}>"}.get(rp, "k_restore_generic")
+    rep = {4: f"vds_ec_jit_restore<{k},{n}>", 3: f"k_restore_syn<{k},{n}>", 2: f"k_restore_bs<{k}>"}.get(
+        rp, "k_restore_generic")
     return enc, rep
 
 
@@ -330,6 +333,8 @@ def main():
 
     vbuild.build()  # a no-op when fresh; build.py serialises concurrent callers
     from vds_amd import chunk
+    if args.no_jit:
+        chunk.jit_set_mode(0)
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -377,7 +382,21 @@ def main():
     for _ in range(args.warmup):
         encode()
         repair()
+    # The survivor set's own restore kernel (vds_amd/csrc/vds_ec_jit.cpp) is
+    # compiled in the background from the set's second use; a repair pass
+    # keeps using it for the rest of the set's objects, so the steady state is
+    # measured with it loaded (untimed here: two uses, the wait, one launch).
+    jit_s = None
+    if not args.no_jit:
+        t_jit = time.perf_counter()
+        repair()
+        repair()
+        chunk.jit_wait()
+        repair()
+        jit_s = time.perf_counter() - t_jit
     torch.cuda.synchronize(dev)
+    restore_kernel = {4: "jit", 3: "syndrome", 2: "bitsliced", 1: "generic"}[chunk.restore_path(k, nodes, L, padding,
+                                                                                             objects)]
     # correctness guard on the measured buffers (outside the timed region)
     assert torch.equal(restored[:size], inp[:size]) and torch.equal(restored[-size:], inp[-size:]), \
         "repair output differs from the input"
@@ -535,6 +554,8 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "traffic_source": traffic_src, "algorithmic_bytes_per_launch": dom_bytes,
                      "avg_launch_ms": round(dom_ms, 4), "kernels": {"encode": enc_name, "repair": rep_name}},
+        "restore_kernel": restore_kernel,
+        "jit_compile_s": round(jit_s, 3) if jit_s is not None else None,
         "align16": align16,
         "live_shape": live,
         "cpu_baseline": None,

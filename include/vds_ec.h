@@ -276,7 +276,9 @@ int vds_ec_save_temp16_host(uint16_t k, uint32_t n, const uint8_t *data, uint64_
  * bench.py and the parity tests (SURVEY.md 8(c) "Input PRNG").               */
 int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void *stream);
 
-/* Which kernel path a device call with these parameters takes: 3 = syndrome
+/* Which kernel path a device call with these parameters takes: 4 = the
+ * survivor set's own run-time compiled kernel (vds_ec_jit_*) for the full
+ * tiles, 3 = syndrome
  * restore (erasure-pattern-independent XOR programs, survivors within
  * 0..k+k/4-1) for the full tiles, 2 = bit-sliced fast path for the full tiles
  * (+ generic tail; objects under one tile whose stripes are whole 512-stripe
@@ -292,6 +294,28 @@ int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size
  * 1 = generic path only.                                                    */
 int vds_ec_regenerate16_path(uint16_t k, const uint16_t *nodes, const uint16_t *targets, uint32_t ntargets,
                              uint64_t chunk_size);
+
+/* ------------------------------------------- run-time compiled restore kernels
+ * A restore whose survivors are k distinct points of 0..k+k/4-1 (k in {16,
+ * 32}) runs k_restore_syn: fixed syndrome programs plus a runtime recovery of
+ * the erased points.  For each such survivor set a device restore meets, the
+ * library also generates the set's own XOR programs (the erased points below
+ * k as fixed combinations of the survivors) and, from the set's second use,
+ * compiles that kernel in the background (hiprtc, gfx950); later restores of
+ * the set use it.  Same bytes.  Mode (vds_ec_jit_set_mode, initially from
+ * VDS_EC_JIT): 0 = off (VDS_EC_JIT=0), 1 = background (default), 2 = compile
+ * on the calling thread at the first use (VDS_EC_JIT=sync).
+ * No counterpart in the reference (its restore is a CPU loop, chunk.h:402-444).
+ *
+ * vds_ec_jit_wait:    block until no compile is queued or running.
+ * vds_ec_jit_build16: compile the kernel of survivor set `nodes` and return
+ *                     its code object size (no device needed; EINVAL for a set
+ *                     the syndrome kernel does not serve, EHIP if hiprtc fails).
+ * vds_ec_jit_ready16: 1 when that set's kernel is compiled, else 0.          */
+int vds_ec_jit_set_mode(int mode);
+int vds_ec_jit_wait(void);
+int vds_ec_jit_build16(uint16_t k, const uint16_t *nodes, uint64_t *code_bytes);
+int vds_ec_jit_ready16(uint16_t k, const uint16_t *nodes);
 
 #ifdef __cplusplus
 }

@@ -44,7 +44,11 @@ def vds_lib():
     from vds_amd import build
     build.build()
     from vds_amd import _lib
-    return _lib.lib()
+    lib = _lib.lib()
+    # run-time compiled restore kernels off, so every test sees the path it
+    # asserts; tests/test_jit_gpu.py switches them on
+    lib.vds_ec_jit_set_mode(0)
+    return lib
 
 
 @pytest.fixture(scope="session")

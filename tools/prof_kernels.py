@@ -18,7 +18,10 @@ p.add_argument("--objects", type=int, default=64)
 p.add_argument("--iters", type=int, default=3)
 p.add_argument("--only", default="")
 p.add_argument("--replica-align", type=int, default=256, help="replica stride alignment (bench.py's default)")
+p.add_argument("--no-jit", action="store_true", help="repair on k_restore_syn (no survivor-set kernel)")
 a = p.parse_args()
+if a.no_jit:
+    chunk.jit_set_mode(0)
 k, n = a.k, a.k + a.m
 size = 64 << 20
 L = chunk.replica_size(k, size)
@@ -32,6 +35,10 @@ erased = list(range(0, n, n // a.m))[: a.m]
 nodes = [r for r in range(n) if r not in erased]
 rp = [reps[i].data_ptr() for i in range(n)]
 chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, rp, Ls)
+if a.only != "encode" and not a.no_jit:  # the survivor set's own kernel, as bench.py measures it
+    for _ in range(2):
+        chunk.restore_device(k, nodes, [reps[r].data_ptr() for r in nodes], L, Ls, size % (2 * k), a.objects, out, size)
+    chunk.jit_wait()
 for _ in range(a.iters):
     if a.only != "restore":
         chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, rp, Ls)

@@ -5,7 +5,7 @@
 
 #include "../../include/vds_ec.h"
 #include "../../vds_amd/csrc/gf_common.hpp"
-#include "paar.hpp"
+#include "../../vds_amd/csrc/xorprog.hpp"
 
 using namespace vds_ec;
 

@@ -69,6 +69,10 @@ SIGNATURES = {
     "vds_ec_fill_splitmix_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]),
     "vds_ec_encode16_path": (C.c_int, [C.c_uint16, u16p, C.c_uint32, C.c_uint64]),
     "vds_ec_restore16_path": (C.c_int, [C.c_uint16, u16p, C.c_uint64, C.c_uint16, C.c_uint32]),
+    "vds_ec_jit_set_mode": (C.c_int, [C.c_int]),
+    "vds_ec_jit_wait": (C.c_int, []),
+    "vds_ec_jit_build16": (C.c_int, [C.c_uint16, u16p, u64p]),
+    "vds_ec_jit_ready16": (C.c_int, [C.c_uint16, u16p]),
     "vds_ec_restore16_batch_device": (C.c_int, [C.c_uint16, C.c_uint32, u16p, vpp, u64p, u16p, vpp, C.c_uint,
                                                 C.c_void_p]),
     "vds_ec_regenerate16_batch_device": (C.c_int, [C.c_uint16, C.c_uint32, u16p, vpp, u64p, C.c_uint32, u16p, vpp,

@@ -23,11 +23,18 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvds_ec.so")
+JITC = os.path.join(HERE, "vds_ec_jitc")  # the run-time kernel compiler (vds_ec_jitc.cpp), next to the library
 LOCK = os.path.join(HERE, ".build.lock")
 # one translation unit per kernel family, compiled in parallel
 SOURCES = ["ec_generic.hip", "ec_encode.hip", "ec_restore_bs.hip", "ec_restore_syn.hip", "sha256.hip",
-           "vds_ec_api.cpp", "vds_ec_wire.cpp"]
-HEADERS = ["bitslice.hpp", "gf_common.hpp", "ec_internal.hpp", "ec_device.hpp"]
+           "vds_ec_api.cpp", "vds_ec_wire.cpp", "vds_ec_jit.cpp"]
+HEADERS = ["bitslice.hpp", "gf_common.hpp", "ec_internal.hpp", "ec_device.hpp", "restore_syn.hpp", "xorprog.hpp",
+           "vds_ec_jitc.cpp"]
+# The device sources the run-time kernels are compiled from (vds_ec_jit.cpp,
+# hiprtc in the helper vds_ec_jitc), embedded in the helper as jit_embed.inc
+# (written into the build directory).
+JIT_FILES = ["gf_common.hpp", "bitslice.hpp", "ec_internal.hpp", "ec_device.hpp", "restore_syn.hpp",
+             "generated/restore_16_20_w4.inc", "generated/restore_32_40_w8.inc"]
 ARCH = os.environ.get("VDS_EC_ARCH", "gfx950")
 
 
@@ -47,15 +54,31 @@ def _deps() -> list[str]:
 
 
 def _stale(lib: str) -> bool:
-    if not os.path.exists(lib):
+    if not os.path.exists(lib) or (lib == LIB and not os.path.exists(JITC)):
         return True
     t = os.path.getmtime(lib)
     return any(os.path.getmtime(d) > t for d in _deps())
 
 
-def compile_cmd(src: str, obj: str, defines: tuple[str, ...] = ()) -> list[str]:
+def write_jit_embed(out_dir: str) -> None:
+    """jit_embed.inc: kJitFiles[] = {include name, text} of JIT_FILES."""
+    delim = "vdsjit"
+    parts = ["static const EmbeddedFile kJitFiles[] = {\n"]
+    for name in JIT_FILES:
+        with open(os.path.join(CSRC, name)) as f:
+            text = f.read()
+        if ")" + delim + '"' in text:
+            raise RuntimeError(f"{name} contains the raw-string delimiter")
+        parts.append(f'    {{"{name}", R"{delim}({text}){delim}"}},\n')
+    parts.append("};\n")
+    with open(os.path.join(out_dir, "jit_embed.inc"), "w") as f:
+        f.write("".join(parts))
+
+
+def compile_cmd(src: str, obj: str, defines: tuple[str, ...] = (), includes: tuple[str, ...] = ()) -> list[str]:
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-c", *defines,
-           "-I", os.path.join(ROOT, "include"), os.path.join(CSRC, src), "-o", obj]
+           "-I", os.path.join(ROOT, "include"), *[a for d in includes for a in ("-I", d)],
+           os.path.join(CSRC, src), "-o", obj]
     if src.endswith(".cpp"):
         cmd[1:1] = ["-x", "hip"]
     return cmd
@@ -63,6 +86,7 @@ def compile_cmd(src: str, obj: str, defines: tuple[str, ...] = ()) -> list[str]:
 
 def _compile_all(tmp: str, defines: tuple[str, ...], verbose: bool) -> list[str]:
     jobs = []
+    write_jit_embed(tmp)
     for src in SOURCES:
         obj = os.path.join(tmp, src.rsplit(".", 1)[0] + ".o")
         cmd = compile_cmd(src, obj, defines)
@@ -70,8 +94,13 @@ def _compile_all(tmp: str, defines: tuple[str, ...], verbose: bool) -> list[str]
             print(" ".join(cmd), file=sys.stderr)
         jobs.append((cmd, obj))
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 1), 8))
+    rocm = os.path.dirname(os.path.dirname(os.path.realpath(_hipcc())))
+    jitc = [_hipcc(), "-O2", "-std=c++20", "-I", tmp, os.path.join(CSRC, "vds_ec_jitc.cpp"), "-o",
+            os.path.join(tmp, "vds_ec_jitc"), f"-L{rocm}/lib", "-lhiprtc", f"-Wl,-rpath,{rocm}/lib",
+            "-Wl,--disable-new-dtags"]
     with cf.ThreadPoolExecutor(workers) as ex:
         futs = [ex.submit(subprocess.run, cmd, check=True) for cmd, _ in jobs]
+        futs.append(ex.submit(subprocess.run, jitc, check=True))
         for f in futs:
             f.result()
     return [obj for _, obj in jobs]
@@ -95,7 +124,9 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None,
                 objs = _compile_all(tmp, defines, verbose)
                 tmp_lib = os.path.join(tmp, "lib.so")
                 subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp_lib] + objs +
-                               ["-lpthread"], check=True)
+                               ["-lpthread", "-ldl"], check=True)
+                os.replace(os.path.join(tmp, "vds_ec_jitc"), os.path.join(os.path.dirname(os.path.abspath(lib)),
+                                                                        "vds_ec_jitc"))
                 os.replace(tmp_lib, lib)
         finally:
             fcntl.flock(lk, fcntl.LOCK_UN)

@@ -471,6 +471,39 @@ def upload(req_id: int, body_b64, k: int = 32, n: int = 64):
             "json": upload_response_json(req_id, names, data_hash, rsize)}
 
 
+def restore_path(k: int, nodes: Sequence[int], chunk_size: int, padding: int = 0, count: int = 1) -> int:
+    """vds_ec_restore16_path: 4 = the survivor set's run-time compiled kernel,
+    3 = k_restore_syn, 2 = k_restore_bs, 1 = generic only."""
+    a = _ids(nodes, 2)
+    return int(_lib.lib().vds_ec_restore16_path(k, _idp(a, 2), chunk_size, padding, count))
+
+
+def jit_set_mode(mode: int) -> None:
+    """0 = off, 1 = background compiles from a survivor set's second use
+    (default), 2 = compile at the first use (vds_ec_jit_set_mode)."""
+    check(_lib.lib().vds_ec_jit_set_mode(mode))
+
+
+def jit_wait() -> None:
+    """Block until the library's run-time compiles of survivor-set-specific
+    restore kernels (vds_ec_jit_*) are done."""
+    check(_lib.lib().vds_ec_jit_wait())
+
+
+def jit_build(k: int, nodes: Sequence[int]) -> int:
+    """Compile (no device needed) the restore kernel of survivor set `nodes`;
+    returns its code object size."""
+    a = _ids(nodes, 2)
+    out = C.c_uint64(0)
+    check(_lib.lib().vds_ec_jit_build16(k, _idp(a, 2), C.byref(out)))
+    return out.value
+
+
+def jit_ready(k: int, nodes: Sequence[int]) -> bool:
+    a = _ids(nodes, 2)
+    return bool(_lib.lib().vds_ec_jit_ready16(k, _idp(a, 2)))
+
+
 def fill_splitmix_device(dst, size: int, seed: int, stream=None) -> None:
     ptr = dst.data_ptr() if hasattr(dst, "data_ptr") else int(dst)
     check(_lib.lib().vds_ec_fill_splitmix_device(ptr, size, seed, _stream_ptr(stream)), "fill_splitmix")

@@ -12,8 +12,6 @@
 // reference (big-endian 16-bit cells, binary_serialize.cpp:18-22).
 #pragma once
 
-#include <utility>
-
 #include "gf_common.hpp"
 
 #if defined(__HIPCC__) || defined(__HIP__)
@@ -179,8 +177,13 @@ VDS_INLINE uint32_t fold_row(uint32_t v, const Plane16 &acc) {
     return v;
 }
 
-template <uint32_t C, size_t... I>
-VDS_INLINE Plane16 row_horner_impl(const Plane16 &acc, const Plane16 &x, std::index_sequence<I...>) {
+// (an integer sequence of our own: the kernels also compile under hiprtc,
+// which has no standard library headers)
+template <class T, T... I>
+struct IntSeq {};
+
+template <uint32_t C, int... I>
+VDS_INLINE Plane16 row_horner_impl(const Plane16 &acc, const Plane16 &x, IntSeq<int, I...>) {
   Plane16 out;
   ((out.p[I] = fold_row<C, (int)I, 0>(x.p[I], acc)), ...);
   return out;
@@ -197,7 +200,7 @@ VDS_INLINE Plane16 plane_horner_rows(const Plane16 &acc, const Plane16 &x) {
   if constexpr (C == 0)
     return x;
   else
-    return row_horner_impl<C>(acc, x, std::make_index_sequence<16>{});
+    return row_horner_impl<C>(acc, x, __make_integer_seq<IntSeq, int, 16>{});
 }
 
 // Multiply by a wave-uniform runtime constant c (< 2^16): Horner over all 16

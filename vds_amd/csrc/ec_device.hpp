@@ -3,11 +3,13 @@
 // Internal to libvds_ec.so.
 #pragma once
 
+#ifndef __HIPCC_RTC__  // (hiprtc: device code only, vds_ec_jit.cpp)
 #include <hip/hip_runtime.h>
 
 #include <atomic>
-#include <cstdint>
 #include <cstdlib>
+#endif
+#include <cstdint>
 
 #include "bitslice.hpp"
 #include "ec_internal.hpp"
@@ -110,6 +112,7 @@ __device__ __forceinline__ TileRange tile_range(uint32_t total) {
 }
 
 // ------------------------------------------------------------ host helpers
+#ifndef __HIPCC_RTC__
 
 // Study override of a fast kernel's grid (workgroups), read once per launcher:
 // VDS_EC_ENC_GRID / VDS_EC_SYN_GRID (0 or unset = the default sizing).
@@ -133,5 +136,7 @@ hipError_t ensure_lds_attr(Kernel *k, int bytes) {
   if (e == hipSuccess && dev >= 0 && dev < kMaxDev) done[dev].store(1, std::memory_order_release);
   return e;
 }
+
+#endif  // __HIPCC_RTC__
 
 }  // namespace vds_ec

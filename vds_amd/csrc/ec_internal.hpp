@@ -2,7 +2,9 @@
 // the kernels (ec_generic.hip, ec_encode.hip, ec_restore_bs.hip, ec_restore_syn.hip).  Internal to libvds_ec.so.
 #pragma once
 
+#ifndef __HIPCC_RTC__  // (hiprtc sees the launch structs only: vds_ec_jit.cpp)
 #include <hip/hip_runtime_api.h>
+#endif
 
 #include <cstdint>
 
@@ -218,6 +220,7 @@ struct RegenTailArgs {  // one survivor set, `count` objects at strides, any k
   uint8_t *outs[kMaxLaunchReplicas];
   uint64_t out_stride;
 };
+#ifndef __HIPCC_RTC__
 hipError_t launch_regen_tail(const RegenTailArgs &a, hipStream_t s);
 // The batched k_restore_syn regenerate's objects objs[0..count) (device
 // tables of the batch launch; survivor points from their plans, targets the
@@ -241,6 +244,12 @@ bool has_restore_syn(uint32_t k, uint32_t n);
 // W[j][a] = v_a a^j of the syndrome map for (k, n); nullptr if not compiled.
 const uint16_t *restore_syn_weights(uint32_t k, uint32_t n);
 hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen = false);
+// The run-time compiled restore kernel of a's survivor set (vds_ec_jit.cpp) on
+// the current device, or nullptr (disabled, not compiled yet -- then queued --
+// or failed): a.point[0..k) set by the plan.
+hipFunction_t jit_restore_function(uint32_t k, uint32_t n, const SynRestoreArgs &a);
+bool jit_enabled();  // mode != 0 (vds_ec_jit_set_mode)
+hipError_t launch_restore_syn_jit(hipFunction_t fn, uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s);
 // a.objs / a.plans / a.tiles / a.total_tiles set; the other fields unused
 hipError_t launch_restore_syn_batch(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen);
 hipError_t launch_regen_generic(const RegenArgs &a, hipStream_t s);
@@ -257,5 +266,7 @@ hipError_t launch_fill_splitmix(uint8_t *dst, uint64_t size, uint64_t seed, hipS
 // Device -> mapped pinned host copy by a kernel (dst: the device view of the
 // host buffer; both 16-byte aligned).
 hipError_t launch_push(uint8_t *dst_host_dev, const uint8_t *src, uint64_t bytes, hipStream_t s);
+
+#endif  // __HIPCC_RTC__
 
 }  // namespace vds_ec

@@ -11,7 +11,9 @@
 // against the compiled reference gf.h.
 #pragma once
 
+#ifndef __HIPCC_RTC__  // (hiprtc: the restore kernels compiled at run time, vds_ec_jit.cpp)
 #include <cstddef>
+#endif
 #include <cstdint>
 
 #if defined(__HIPCC__) || defined(__HIP__)

@@ -1,0 +1,896 @@
+// restore_syn.hpp -- the k_restore_syn kernel body (ec_restore_syn.hip), in a
+// header of its own so that vds_ec_jit.cpp can compile pattern-specific
+// instantiations of it at run time (hiprtc) from the same source.
+//
+// Restore of an object from any K of its N replicas without a per-pattern
+// K x K inverse (chunk_restore<uint16_t>::restore, chunk.h:290-444; the
+// BASELINE configs (16, 20) and (32, 40)).  The generated RestorePrograms<K,
+// N, WV> specialisations (generated/restore_K_N_wW.inc) must be included
+// before the body is instantiated.
+#pragma once
+
+#include "ec_device.hpp"
+
+namespace vds_ec {
+
+constexpr int64_t kNoBound = 0x7FFFFFFFFFFFFFFFll;
+
+template <int K, int N, int WV> struct RestorePrograms;
+
+// k_restore_syn<K, N, WV>: one 2048-stripe tile per workgroup of WV waves.
+// Two such workgroups share a CU (k = 16); their phases drift apart, so one
+// workgroup's barrier waits and memory phases overlap the other's VALU.  (Two
+// tiles per 8-wave workgroup, which keeps the two waves of a SIMD in the same
+// phase, measured slower: repair 1597 -> 1478-1486 GiB/s at 512 objects.)
+template <int K, int N, int WV>
+struct SynShape {
+  static constexpr int kWaves = WV;
+  static constexpr int kThreads = 64 * WV;
+  static constexpr int kM = N - K;
+  static constexpr int kLoadPer = K / WV;          // survivors loaded per wave
+  using P = RestorePrograms<K, N, WV>;
+  static constexpr int kSynRows = P::kSynRows;     // syndrome bit-rows per wave
+  static constexpr int kCells = P::kIntRows / 16;  // object cells per wave
+  // group-major LDS: plane p = 16 point + bit lives in group p / 4; the four
+  // planes of a group are one 16-byte word per lane, so every access is a
+  // conflict-free ds_{read,write}_b128 (byte (p/4)*1024 + lane*16 + 4*(p%4))
+  static constexpr int kLdsBytes = N * 16 * 64 * 4;
+  static constexpr int kWavesPerSimd = (160 * 1024 / kLdsBytes) * WV / 4;
+  static constexpr bool kPrio = 160 * 1024 / kLdsBytes >= 2;  // phase priorities (syn_prio)
+  static_assert(K % WV == 0 && kM <= WV, "survivor loads and erased slots must map onto waves");
+  static_assert(kSynRows == 16 && kM == WV, "scatter recovery needs one whole syndrome per wave");
+  static_assert(kCells == 2 || kCells == 4, "row split must be b128 / word-group aligned");
+  static_assert(kLdsBytes <= 160 * 1024, "LDS");
+};
+
+// Diagnostic build (VDS_DIAG_STAMPS=1, timing only): every wave of
+// k_restore_syn accumulates s_memtime deltas per phase of its tiles into
+// g_syn_stamps[block][wave][phase] (read with vds_ec_diag_stamps; phases in
+// tools/syn_stamps.py).  The marks wait for outstanding scalar and LDS
+// operations and the compiler may move VALU work across them: read the
+// barrier waits, not the exact split of neighbouring phases.  Off: the marks
+// compile to nothing.  tests/test_build.py compile-checks this build.
+#ifndef VDS_DIAG_STAMPS
+#define VDS_DIAG_STAMPS 0
+#endif
+
+// Wave priority by phase when two workgroups share a CU (k = 16).  Their
+// phases drift apart; the workgroup in stage 1 (survivors -> LDS planes) and
+// stage A runs at priority 1, and the one transposing and staging its output
+// at 2, so the other workgroup's long XOR programs fill the gaps instead of
+// delaying the phases that end in a barrier of all four waves.  Same-box A/B,
+// 512 x 64 MiB: repair 18.65 -> 16.54-16.59 ms (+12%), again on a second box
+// 19.0-19.25 -> 16.9-17.0 ms.  Also measured: priority on the copy-out stores
+// (neutral), on stage 1 alone (+1.6%), staging alone (+0.5%), the syndrome
+// programs or stage B or C as well (less gain; every phase at 1 is the
+// default again); stage C at 1 or every level one higher (1 -> 2, 2 -> 3):
+// within 1%.  One workgroup per CU (k = 32): neutral, not used.
+template <int PRIO, bool ON>
+__device__ __forceinline__ void syn_prio() {
+  if constexpr (ON) __builtin_amdgcn_s_setprio(PRIO);
+}
+
+#if VDS_DIAG_STAMPS
+constexpr int kStampPhases = 20;
+constexpr int kStampSlots = 4096 * 4 * kStampPhases;
+__device__ unsigned long long g_syn_stamps[kStampSlots];
+struct Stamps {
+  uint64_t prev, acc[kStampPhases];
+  __device__ __forceinline__ void init() {
+    prev = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < kStampPhases; ++i) acc[i] = 0;
+  }
+  __device__ __forceinline__ void mark(int i) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    acc[i] += now - prev;
+    prev = now;
+  }
+  __device__ __forceinline__ void flush(int slot, int lane) {
+    if (lane == 0 && slot < 4096 * 4)
+      for (int i = 0; i < kStampPhases; ++i) g_syn_stamps[slot * kStampPhases + i] = acc[i];
+  }
+};
+#else
+struct Stamps {
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void flush(int, int) {}
+};
+#endif
+
+// Group g of the plane-major LDS as seen by one lane.  ds_read_b128 carries a
+// 16-bit immediate offset, so groups past 64 KiB (points >= 16) are addressed
+// from a second base register; the base is laundered through an empty asm so
+// the compiler does not fold it back into one address register per group.
+struct SynLds {
+  lds_char *base;
+  uint32_t lo;   // 16 * lane
+  uint32_t hi;   // 16 * lane + 64 KiB (opaque)
+  uint32_t hi2;  // 16 * lane + 128 KiB (opaque; points 32.. of k = 32)
+  // A compile-time group is an immediate offset (< 64 KiB) from one of the
+  // three bases, so no per-group address register stays live; a runtime
+  // group costs one address add.
+  __device__ __forceinline__ lds_char *at(int g) const {
+    if (__builtin_constant_p(g)) {
+      if (g < 64) return base + lo + g * 1024;
+      if (g < 128) return base + hi + (g - 64) * 1024;
+      return base + hi2 + (g - 128) * 1024;
+    }
+    return base + lo + g * 1024;
+  }
+  __device__ __forceinline__ u32x4 operator()(int g) const { return *(lds_v4 *)at(g); }
+  __device__ __forceinline__ void put(int g, u32x4 v) const { *(lds_v4 *)at(g) = v; }
+};
+
+__device__ __forceinline__ void syn_put_point(const SynLds &L, int pt, const uint32_t (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) L.put(4 * pt + g, u32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]});
+}
+
+__device__ __forceinline__ void syn_get_point(const SynLds &L, int pt, uint32_t (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const u32x4 x = L(4 * pt + g);
+    v[4 * g] = x[0];
+    v[4 * g + 1] = x[1];
+    v[4 * g + 2] = x[2];
+    v[4 * g + 3] = x[3];
+  }
+}
+
+// Interpolation from the fixed points F = {0..K-1} by one level of the
+// additive FFT (Gao-Mateer).  F is the GF(2)-span of 1, x, x^2, x^3 (, x^4),
+// so with G = {0, 2, .., K-2} and s(X) = X^2 + X (which maps g and g+1 to the
+// same point):
+//   P(X) = P0(s(X)) + X P1(s(X)),  deg P0, P1 < K/2,
+//   P1(s(g)) = c_g + c_{g+1},  P0(s(g)) = c_g + g P1(s(g)).
+// Stage A forms those K/2 value pairs in place (Q0 -> slot g, Q1 -> slot g+1),
+// stage B interpolates P0 and P1 on D = s(G) with generated XOR programs
+// (RestorePrograms::interpB), and stage C expands (X^2+X)^i = X^i (X+1)^i,
+// whose coefficients are binomials mod 2, so it is XORs only.  About 60% of
+// the XORs of the direct 16-point program (1375 vs 1280 GiB/s).
+template <int W, int NP, int Q = 0>
+__device__ __forceinline__ void syn_gm_stage_a(const SynLds &L) {
+  if constexpr (Q < NP) {
+    constexpr int i = NP * W + Q;  // the pair (g, g + 1) = (2 i, 2 i + 1)
+    Plane16 c0, c1;
+    syn_get_point(L, 2 * i, c0.p);
+    syn_get_point(L, 2 * i + 1, c1.p);
+    const Plane16 q1 = plane_xor(c0, c1);
+    const Plane16 q0 = plane_horner_rows<(uint32_t)(2 * i)>(q1, c0);
+    syn_put_point(L, 2 * i, q0.p);
+    syn_put_point(L, 2 * i + 1, q1.p);
+    syn_gm_stage_a<W, NP, Q + 1>(L);
+  }
+}
+
+// Output cell k = sum of P0_i with C(i, k - i) odd and of P1_i with
+// C(i, k - 1 - i) odd (Lucas: C(i, m) is odd iff the bits of m are a subset of
+// those of i).  P0_i sits in LDS slot i, P1_i in slot K/2 + i.
+template <int K, int W, int NC>
+__device__ __forceinline__ void syn_gm_stage_c(const SynLds &L, uint32_t (&cells)[16 * NC]) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int k = NC * W + c;
+    uint32_t acc[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) acc[b] = 0u;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const int i = t % (K / 2);
+      const int m = t < K / 2 ? k - i : k - 1 - i;
+      if (m >= 0 && m <= i && (m & ~i) == 0) {
+        uint32_t v[16];
+        syn_get_point(L, t, v);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) acc[b] ^= v[b];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 16; ++b) cells[16 * c + b] = acc[b];
+  }
+}
+
+template <int K, int N, int WV, int W>
+__device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
+  static_assert((K == 16 && WV == 4) || (K == 32 && WV == 8),
+                "the one-level interpolation is laid out for k = 16 and k = 32");
+  using P = RestorePrograms<K, N, WV>;
+  constexpr int kPairs = (K / 2) / WV;           // stage-A pairs per wave
+  constexpr int kHalfCells = P::kHalfRows / 16;  // stage-B cells per wave
+  constexpr int kParts = WV / 2;                 // waves per half-size polynomial
+  constexpr bool kPrio = SynShape<K, N, WV>::kPrio;
+  if constexpr (W < WV) {
+    if (wave != W) return syn_interp_gm<K, N, WV, W + 1>(wave, L, cells, st);
+    syn_prio<1, kPrio>();
+    syn_gm_stage_a<W, kPairs>(L);
+    syn_prio<0, kPrio>();
+    st.mark(7);
+    __syncthreads();
+    st.mark(8);
+    uint32_t half[P::kHalfRows];
+    P::interpB(W, L, half);
+    st.mark(9);
+    __syncthreads();  // every wave has read its Q values
+    st.mark(10);
+    // P0 (W < kParts) or P1 cells kHalfCells (W % kParts) + c -> slot (K/2) (W / kParts) + ..
+#pragma unroll
+    for (int c = 0; c < kHalfCells; ++c) {
+      uint32_t v[16];
+#pragma unroll
+      for (int b = 0; b < 16; ++b) v[b] = half[16 * c + b];
+      syn_put_point(L, (K / 2) * (W / kParts) + kHalfCells * (W % kParts) + c, v);
+    }
+    st.mark(11);
+    __syncthreads();
+    st.mark(12);
+    syn_gm_stage_c<K, W, K / WV>(L, cells);
+    st.mark(13);
+  }
+}
+
+// One coefficient-bit pair of the recovery walk: acc ^= T, T1 or T ^ T1 as
+// the pair's two bits select (two = bit b | bit b+1 << 8), in one asm block
+// with its own branches.  As plain C++ the three arms computed into
+// different registers and every merge block copied the sixteen planes back
+// (8 v_mov_b64 per product and bit pair: as many moves as XORs); here the
+// planes are updated in place.  (The compares write SCC: declared clobbered,
+// or a live SCC of the surrounding code is lost.)
+#define VDS_RS_C(i) [c##i] "+v"(acc.p[i])
+#define VDS_RS_A(i) [a##i] "v"(t.p[i])
+#define VDS_RS_B(i) [b##i] "v"(t1.p[i])
+#define VDS_RS_LIST(M) M(0), M(1), M(2), M(3), M(4), M(5), M(6), M(7), M(8), M(9), M(10), M(11), M(12), M(13), M(14), M(15)
+#define VDS_RS_SEQ(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
+#define VDS_RS_XA(i) "v_xor_b32 %[c" #i "], %[c" #i "], %[a" #i "]\n"
+#define VDS_RS_XB(i) "v_xor_b32 %[c" #i "], %[c" #i "], %[b" #i "]\n"
+#define VDS_RS_X3(i) "v_bitop3_b32 %[c" #i "], %[c" #i "], %[a" #i "], %[b" #i "] bitop3:0x96\n"
+__device__ __forceinline__ void rec_pair(Plane16 &acc, const Plane16 &t, const Plane16 &t1, uint32_t two) {
+  asm volatile(
+      "s_cmp_eq_u32 %[two], 1\n"
+      "s_cbranch_scc0 1f\n" VDS_RS_SEQ(VDS_RS_XA)
+      "s_branch 3f\n"
+      "1:\n"
+      "s_cmpk_eq_u32 %[two], 0x100\n"
+      "s_cbranch_scc0 2f\n" VDS_RS_SEQ(VDS_RS_XB)
+      "s_branch 3f\n"
+      "2:\n"
+      "s_cmpk_eq_u32 %[two], 0x101\n"
+      "s_cbranch_scc0 3f\n" VDS_RS_SEQ(VDS_RS_X3)
+      "3:\n"
+      : VDS_RS_LIST(VDS_RS_C)
+      : VDS_RS_LIST(VDS_RS_A), VDS_RS_LIST(VDS_RS_B), [two] "s"(two)
+      : "scc");
+}
+// RT mode: the same walk with a different coefficient in each half of the
+// tile.  After the stage-1 transpose, bits 0-7 and 16-23 of every plane word
+// hold half 0's stripes and bits 8-15, 24-31 half 1's (kRtH0 / kRtH1), so a
+// coefficient bit is a wave-uniform mask per bit -- 0, kRtH0, kRtH1 or all
+// ones -- and acc ^= (T & ma) ^ (T1 & mb) is one masked v_bitop3 per plane
+// and nonzero mask.  (Seven specialised arms per bit pair, as rec_pair's,
+// made the unrolled walk ~128 KiB of code: it thrashed the instruction cache,
+// 4x slower per tile; one arm per mask value, with the masks preloaded in
+// VGPRs, measured no faster than this copy of the mask: 363 vs 377 GiB/s.)
+// The mask is copied to a VGPR first: a v_bitop3 reading an SGPR issues at
+// ~0.6 of the all-VGPR rate.
+constexpr uint32_t kRtH0 = 0x00FF00FFu, kRtH1 = 0xFF00FF00u;
+#define VDS_RD_MA(i) "v_bitop3_b32 %[c" #i "], %[c" #i "], %[a" #i "], %[tm] bitop3:0x78\n"
+#define VDS_RD_MB(i) "v_bitop3_b32 %[c" #i "], %[c" #i "], %[b" #i "], %[tm] bitop3:0x78\n"
+__device__ __forceinline__ void rec_dual(Plane16 &acc, const Plane16 &t, const Plane16 &t1, uint32_t ma, uint32_t mb) {
+  uint32_t tm;
+  asm volatile(
+      "s_cmp_eq_u32 %[ma], 0\n"
+      "s_cbranch_scc1 1f\n"
+      "v_mov_b32 %[tm], %[ma]\n" VDS_RS_SEQ(VDS_RD_MA)
+      "1:\n"
+      "s_cmp_eq_u32 %[mb], 0\n"
+      "s_cbranch_scc1 2f\n"
+      "v_mov_b32 %[tm], %[mb]\n" VDS_RS_SEQ(VDS_RD_MB)
+      "2:\n"
+      : VDS_RS_LIST(VDS_RS_C), [tm] "=&v"(tm)
+      : VDS_RS_LIST(VDS_RS_A), VDS_RS_LIST(VDS_RS_B), [ma] "s"(ma), [mb] "s"(mb)
+      : "scc");
+}
+#undef VDS_RD_MA
+#undef VDS_RD_MB
+#undef VDS_RS_C
+#undef VDS_RS_A
+#undef VDS_RS_B
+#undef VDS_RS_LIST
+#undef VDS_RS_SEQ
+#undef VDS_RS_XA
+#undef VDS_RS_XB
+#undef VDS_RS_X3
+
+// LDS XOR of a point's sixteen planes (this lane's 64 bytes) as eight
+// ds_xor_b64: planes 4g..4g+3 of point pt at byte (4 pt + g) 1 KiB + 16 lane.
+__device__ __forceinline__ void lds_xor_point(const SynLds &L, int pt, const Plane16 &v) {
+  __attribute__((address_space(3))) uint64_t *dst =
+      (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * pt);
+#pragma unroll
+  for (int h = 0; h < 8; ++h)
+    __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1), (uint64_t)v.p[2 * h] | ((uint64_t)v.p[2 * h + 1] << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Batch mode: the last tile of an object may run past its bytes.  Loads
+// beyond `valid` bytes read zeros and stores beyond it write nothing (byte by
+// byte for the one 16-byte piece that straddles the end).
+__device__ __forceinline__ u32x4 ld16_guard(const uint8_t *p, int64_t valid) {
+  if (valid >= 16) return g_ld<4, u32x4>(p);
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (valid > 0) {  // (chunk lengths are even: whole dwords, then a 2-byte cell)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (4 * i + 4 <= valid) v[i] = *(const gmem<uint32_t> *)(p + 4 * i);
+    if (valid & 2) v[valid >> 2] = *(const gmem<uint16_t> *)(p + (valid & ~3));
+  }
+  return v;
+}
+__device__ __forceinline__ void st16_guard(uint8_t *p, u32x4 v, int64_t valid) {
+  if (valid >= 16) {
+    g_st<8>(p, v);
+  } else if (valid > 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (4 * i + 4 <= valid) *(gmem<uint32_t> *)(p + 4 * i) = v[i];
+    const int w = (int)(valid >> 2);
+    const uint32_t x = v[w];
+    for (int b = 0; b < (int)(valid & 3); ++b) ((gmem<uint8_t> *)p)[4 * w + b] = uint8_t(x >> (8 * b));
+  }
+}
+
+// Restore of an object from any K of its N replicas without a per-pattern
+// K x K inverse (tools/xorgen/gen_restore.cpp).  Per tile, wave w:
+//  1. loads survivors kLoadPer*w.. into their points' planes (waves < M also
+//     zero one erased point);
+//  2. computes syndrome S_w over all N points (erased points read as zero)
+//     and scatters its share of every recovered point into the erased slots;
+//  3. interpolates cells kCells*w.. from the fixed points 0..K-1 and stores
+//     them big-endian.
+// Tiles are strided over each XCD's workgroups (tile_range; one contiguous
+// range of tiles per workgroup measured slower: repair 1572 -> 1460 GiB/s).
+// BATCH: one launch over the tiles of many objects, each with its own
+// survivors, erasure plan, size and output (SynBatchTile / SynBatchObj /
+// SynBatchPlan, read with wave-uniform scalar loads).  Each half of a tile
+// (q = 0, 1 and q = 2, 3 of the loads; waves 0..WV/2-1 and WV/2.. of the
+// copy-out) is a stripe range of its own object; a half that runs past its
+// object's bytes takes the guarded loads and stores.
+// RT (batch only): phase 2 is the runtime-coefficient combination of the
+// slots (SynBatchRt) instead of syndromes + recovery, so any k survivors of
+// any ids serve, a different set in each half of a tile: restore writes the
+// combinations into the borrowed slots' erased points and interpolates as
+// usual; regenerate accumulates row m in LDS slot K + m and stores it as
+// replica bytes.  Each wave combines the slots it loaded (registers) for
+// every row and adds its share with LDS XOR atomics, so the waves split the
+// work evenly whatever the rows.
+// FILL: a pattern-specific program (FillP, generated for one erased set and
+// compiled at run time, vds_ec_jit.cpp) computes the erased points below K
+// straight from the survivors instead of syndromes + recovery.
+struct NoFill {
+  static constexpr int kFill = -1;
+};
+template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false, class FillP = NoFill>
+__device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
+  constexpr bool FILL = FillP::kFill >= 0;
+  using S = SynShape<K, N, WV>;
+  using P = typename S::P;
+  constexpr bool kPrio = S::kPrio;
+  static_assert(!RT || BATCH, "RT is a batch mode");
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const BitMasks bm = bit_masks();
+  SynLds L;
+  L.base = (lds_char *)lds;
+  L.lo = 16u * lane;
+  L.hi = 16u * lane + 65536u;
+  asm volatile("" : "+v"(L.hi));
+  if constexpr (N * 16 > 128) {
+    L.hi2 = 16u * lane + 131072u;
+    asm volatile("" : "+v"(L.hi2));
+  } else {
+    L.hi2 = L.hi;
+  }
+  // per-tile data: the launch's (uniform), or in batch mode the tile
+  // record's (t and wave are uniform, so the s_ld reads are scalar loads)
+  auto obj_of = [&](uint32_t t) -> uint32_t { return t / a.tiles_per_obj; };
+  auto stripe0_of = [&](uint32_t t) -> uint64_t { return (uint64_t)(t % a.tiles_per_obj) * kTileStripes; };
+  auto half_obj = [&](uint32_t t, int h) -> const SynBatchObj & { return a.objs[s_ld(&a.tiles[t].obj[h])]; };
+  auto half_s0 = [&](uint32_t t, int h) -> uint64_t { return s_ld(&a.tiles[t].stripe0[h]); };
+
+  // survivor staging: the next tile's loads are issued after the syndrome
+  // programs (k = 32: after the interpolation, see kLateLoad) and land while
+  // the rest of this tile runs
+  u32x4 Q[S::kLoadPer][4];
+  auto load = [&](uint32_t t) {
+    if constexpr (BATCH) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const SynBatchObj &d = half_obj(t, h);
+        const uint64_t st0 = half_s0(t, h);
+        // bytes of each survivor from this half's first cell on
+        const int64_t valid = (int64_t)s_ld(&d.chunk_len) - (int64_t)(2 * st0);
+        const uint8_t *src[S::kLoadPer];
+#pragma unroll
+        for (int s = 0; s < S::kLoadPer; ++s) src[s] = s_ld(&d.chunks[wave * S::kLoadPer + s]) + 2 * st0 + 16 * lane;
+        if (valid >= 2 * (int64_t)kHalfStripes) {
+#pragma unroll
+          for (int s = 0; s < S::kLoadPer; ++s)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) Q[s][2 * h + q] = g_ld<4, u32x4>(src[s] + 1024 * q);
+        } else {
+#pragma unroll
+          for (int s = 0; s < S::kLoadPer; ++s)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) Q[s][2 * h + q] = ld16_guard(src[s] + 1024 * q, valid - 16 * lane - 1024 * q);
+        }
+      }
+    } else {
+      const uint32_t ob = obj_of(t);
+      const uint64_t st0 = stripe0_of(t);
+#pragma unroll
+      for (int s = 0; s < S::kLoadPer; ++s) {
+        const uint8_t *src = a.chunks[wave * S::kLoadPer + s] + (uint64_t)ob * a.chunk_stride + 2 * st0 + 16 * lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Q[s][q] = g_ld<4, u32x4>(src + 1024 * q);
+      }
+    }
+  };
+  // The next tile's survivors, or zeros past the last tile: both paths define
+  // Q, so the values consumed by this tile's stage 1 die there instead of
+  // staying live (as loop-carried state) through the programs until the load
+  // (k = 32 spilled 203 VGPRs that way: 1.6x / 1.4x the algorithmic traffic).
+  const TileRange tr = tile_range(a.total_tiles);
+  auto prefetch = [&](uint32_t t) {
+    if (t < tr.end) {
+      load(t);
+    } else {
+#pragma unroll
+      for (int s = 0; s < S::kLoadPer; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Q[s][q] = u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  Stamps st;
+  st.init();
+  // k = 32 (one 160 KiB workgroup per CU): the prefetched survivors would be
+  // live across the syndrome and stage-B programs, which then spill; they are
+  // issued after the interpolation instead and land under the staging and
+  // stores (REGEN has no interpolation and keeps the early issue)
+  // (batch: the guarded loads and descriptor addresses would not fit beside
+  // the programs either)
+  // (RT: this wave's slots stay in registers through phase 2; the regenerate
+  // branch issues its prefetch there)
+  constexpr bool kLateLoad = ((K == 32 || BATCH) && !REGEN) || RT;
+  const uint32_t t_step = tr.step;
+  prefetch(tr.first);
+  // vmcnt counts loads and stores together and retires them in issue order.
+  // In the loop, the 16 copy-out stores of a tile are issued after the next
+  // tile's survivor loads, so the loads can be waited for with vmcnt(16 + ..)
+  // while the stores drain.  The compiler's wait insertion merges the loop's
+  // entry and back-edge states by the youngest position of each pending
+  // register: at the entry the prefetched loads ARE the youngest ops, so it
+  // would wait vmcnt(<16) at the top of every tile -- for the previous tile's
+  // stores to complete.  Issuing the same 16 stores here (zeros into this
+  // wave's copy-out chunk of its first tile, which that tile's copy-out
+  // overwrites, in order, from the same wave) makes both states alike.
+  if constexpr (!REGEN && !BATCH) {  // (batch: guarded stores; nothing to mirror)
+    if (tr.first < tr.end) {
+      const uint32_t t0 = tr.first;
+      uint8_t *g0 = a.out + (uint64_t)(t0 / a.tiles_per_obj) * a.out_stride +
+                    (uint64_t)(t0 % a.tiles_per_obj) * kTileStripes * (2 * K) + 16384u * wave + 16u * lane;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) g_st<8>(g0 + 1024 * i, u32x4{0u, 0u, 0u, 0u});
+    }
+  }
+  for (uint32_t tile = tr.first; tile < tr.end; tile += t_step) {
+    const uint32_t o = BATCH ? 0u : obj_of(tile);  // (non-batch)
+    const uint64_t stripe0 = BATCH ? 0u : stripe0_of(tile);
+    const SynBatchPlan *pl = (BATCH && !RT) ? &a.plans[s_ld(&a.tiles[tile].plan)] : nullptr;
+    auto erased_of = [&](int m) -> int { return (int)s_ld_u8(BATCH ? pl->erased : a.erased, m); };
+    // the LDS point this wave zeroes and (regenerate) stores: an erased point,
+    // or RT regenerate's row slot K + wave
+    const int my_erased = RT ? K + wave : (wave < S::kM ? erased_of(wave) : 0);
+    Plane16 Ps[RT ? S::kLoadPer : 1];  // RT: this wave's slots, kept for phase 2
+    // ---- 1. survivors -> planes of their points; waves < M zero one erased point
+    syn_prio<1, kPrio>();
+    {
+      if (wave < S::kM && (!RT || REGEN) && !FILL) {
+        const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) L.put(4 * my_erased + g, z);
+      }
+      uint64_t bor[2] = {0, 0};  // RT restore: borrowed slots of each half
+      if constexpr (RT && !REGEN) {
+        bor[0] = s_ld(&half_obj(tile, 0).rt.borrowed);
+        bor[1] = s_ld(&half_obj(tile, 1).rt.borrowed);
+      }
+#pragma unroll
+      for (int s = 0; s < S::kLoadPer; ++s) {
+        uint32_t W[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) W[4 * q + d] = Q[s][q][d];
+        transpose16x2(W, bm);  // W[x] = plane of cell bit x^8
+        uint32_t Pl[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) Pl[b] = W[b ^ 8];
+        if constexpr (RT) {
+          const int j = wave * S::kLoadPer + s;
+#pragma unroll
+          for (int b = 0; b < 16; ++b) Ps[s].p[b] = Pl[b];
+          if constexpr (!REGEN) {
+            // slot j as point j: a borrowed half keeps zeros there (its
+            // erased point's value is added in phase 2)
+            const uint32_t keep = (((bor[0] >> j) & 1u) ? 0u : kRtH0) | (((bor[1] >> j) & 1u) ? 0u : kRtH1);
+            if (keep != 0xFFFFFFFFu)
+#pragma unroll
+              for (int b = 0; b < 16; ++b) Pl[b] &= keep;
+            syn_put_point(L, j, Pl);
+          }
+        } else {
+          syn_put_point(L, (int)s_ld_u8(BATCH ? pl->point : a.point, wave * S::kLoadPer + s), Pl);
+        }
+      }
+    }
+    syn_prio<0, kPrio>();
+    st.mark(0);
+    __syncthreads();
+    st.mark(1);
+    uint32_t rt_rows = 0;  // RT: rows of this tile
+    if constexpr (RT) {
+      // ---- 2'. row m of each half = sum_j coef[m][j] * slot j: every wave
+      // combines its own slots (Ps) for all rows, kMC rows per walk of each
+      // slot's x^b chain, and adds its share into the row's LDS point
+      // (restore: the half's erased point epoint[m], masked to the half when
+      // the two halves' points differ; regenerate: slot K + m)
+      const SynBatchObj &d0 = half_obj(tile, 0), &d1 = half_obj(tile, 1);
+      rt_rows = s_ld(&a.tiles[tile].nm);
+      const uint32_t ne0 = s_ld(&d0.rt.ne), ne1 = s_ld(&d1.rt.ne);
+      const uint16_t *cf0 = s_ld(&d0.rt.coef), *cf1 = s_ld(&d1.rt.coef);
+      uint32_t vh0, vh1;  // the half masks in VGPRs (for the scatter)
+      asm("v_mov_b32 %0, %1" : "=v"(vh0) : "i"(kRtH0));
+      asm("v_mov_b32 %0, %1" : "=v"(vh1) : "i"(kRtH1));
+      // two rows per walk of each slot's chain, the pairs in a rolled loop
+      // (code size: see rec_dual)
+      constexpr int kMC = 2;
+#pragma clang loop unroll(disable)
+      for (uint32_t m0 = 0; m0 < rt_rows; m0 += kMC) {
+        Plane16 ce[kMC];
+#pragma unroll
+        for (int m = 0; m < kMC; ++m) ce[m] = plane_zero();
+        // this wave's kLoadPer = 4 slot coefficients of each row, both
+        // halves: 8 contiguous bytes per (half, row), all issued at once
+        static_assert(S::kLoadPer == 4, "one 8-byte scalar load per row and half");
+        uint64_t q0[kMC], q1[kMC];
+#pragma unroll
+        for (int m = 0; m < kMC; ++m) {
+          const uint32_t at = (m0 + m) * K + wave * S::kLoadPer;
+          q0[m] = m0 + m < ne0 ? s_ld(reinterpret_cast<const uint64_t *>(cf0 + at)) : 0ull;
+          q1[m] = m0 + m < ne1 ? s_ld(reinterpret_cast<const uint64_t *>(cf1 + at)) : 0ull;
+        }
+#pragma unroll
+        for (int s = 0; s < S::kLoadPer; ++s) {
+          uint32_t c0[kMC], c1[kMC];
+#pragma unroll
+          for (int m = 0; m < kMC; ++m) {
+            c0[m] = (uint32_t)(q0[m] >> (16 * s)) & 0xFFFFu;
+            c1[m] = (uint32_t)(q1[m] >> (16 * s)) & 0xFFFFu;
+          }
+          // (one slot's chain at a time: interleaving the four independent
+          // chains would not fit beside the accumulators)
+          __builtin_amdgcn_sched_barrier(0);
+          Plane16 tt = Ps[s];
+          // (opaque per row pair: the chains do not depend on m0, and hoisted
+          // out of the loop all 4 x 16 of them spilled)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(tt.p[i]));
+#pragma unroll
+          for (int b = 0; b < 16; b += 2) {
+            __builtin_amdgcn_sched_barrier(0);
+            const Plane16 t1 = plane_mulx(tt);
+#pragma unroll
+            for (int m = 0; m < kMC; ++m) {
+              const uint32_t ma = (((c0[m] >> b) & 1u) ? kRtH0 : 0u) | (((c1[m] >> b) & 1u) ? kRtH1 : 0u);
+              const uint32_t mb = (((c0[m] >> (b + 1)) & 1u) ? kRtH0 : 0u) | (((c1[m] >> (b + 1)) & 1u) ? kRtH1 : 0u);
+              rec_dual(ce[m], tt, t1, ma, mb);
+            }
+            if (b < 14) tt = plane_mulx(t1);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < kMC; ++m) {
+          const uint32_t r = m0 + m;
+          if (r >= rt_rows) break;
+          if constexpr (REGEN) {
+            lds_xor_point(L, K + (int)r, ce[m]);
+          } else {
+            const int p0 = r < ne0 ? (int)s_ld_u8(d0.rt.epoint, (int)r) : -1;
+            const int p1 = r < ne1 ? (int)s_ld_u8(d1.rt.epoint, (int)r) : -1;
+            if (p0 >= 0 && p0 == p1) {
+              lds_xor_point(L, p0, ce[m]);
+            } else {
+              if (p0 >= 0) {
+                Plane16 v;
+#pragma unroll
+                for (int b = 0; b < 16; ++b) v.p[b] = ce[m].p[b] & vh0;
+                lds_xor_point(L, p0, v);
+              }
+              if (p1 >= 0) {
+                Plane16 v;
+#pragma unroll
+                for (int b = 0; b < 16; ++b) v.p[b] = ce[m].p[b] & vh1;
+                lds_xor_point(L, p1, v);
+              }
+            }
+          }
+        }
+      }
+    } else if constexpr (FILL) {
+      if (wave < FillP::kFill) {
+        uint32_t acc[16];
+        FillP::fill(wave, L, acc);
+        syn_put_point(L, FillP::kPoint[wave], acc);
+      }
+      if (!kLateLoad) prefetch(tile + t_step);
+    } else {
+    // ---- 2. wave j holds syndrome S_j whole and scatters its share of every
+    // recovered point, c_e[m] += R[m][j] S_j, into the erased slots (zero since
+    // stage 1) with LDS XOR atomics: T = x^b S_j walks the coefficient bits
+    // once for all M products, and no wave has to gather the syndromes (two
+    // barriers and a park/reload of the syndromes fewer than a gather:
+    // 1384 -> 1525 GiB/s).  The wave-uniform branches measured faster than
+    // their alternatives (512 objects): two separate ifs 1562-1563, masked
+    // v_bitop3 with VGPR masks 1520-1534, against 1573-1577 GiB/s.
+    {
+      Plane16 t;
+      P::syndrome(wave, L, t.p);
+      if (!kLateLoad) prefetch(tile + t_step);
+      st.mark(2);
+      // M <= 4: all products before the barrier (their walk overlaps the
+      // slower waves' syndromes); M = 8: four at a time after it (eight
+      // accumulators would not fit beside the prefetched survivors)
+      constexpr int kMC = S::kM <= 4 ? S::kM : 4;
+      if constexpr (kMC < S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
+#pragma unroll
+      for (int m0 = 0; m0 < S::kM; m0 += kMC) {
+        Plane16 ce[kMC];
+#pragma unroll
+        for (int m = 0; m < kMC; ++m) ce[m] = plane_zero();
+        Plane16 t_copy;  // several chunks walk from the same syndrome
+        Plane16 &tt = kMC < S::kM ? (t_copy = t, t_copy) : t;
+#pragma unroll
+        for (int b = 0; b < 16; b += 2) {
+          const Plane16 t1 = plane_mulx(tt);
+#pragma unroll
+          for (int m = 0; m < kMC; ++m) {
+            const uint32_t sel = BATCH ? s_ld(&pl->solve_sel[m0 + m][b >> 2]) : a.solve_sel[m0 + m][b >> 2];
+            const uint32_t two = (sel >> (8 * (b & 3) + wave)) & 0x101u;
+            rec_pair(ce[m], tt, t1, two);
+          }
+          if (b < 14) tt = plane_mulx(t1);
+        }
+        st.mark(3);
+        if constexpr (kMC == S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
+        st.mark(4);
+#pragma unroll
+        for (int m = 0; m < kMC; ++m) lds_xor_point(L, erased_of(m0 + m), ce[m]);
+      }
+    }
+    }  // (phase 2)
+    st.mark(5);
+    __syncthreads();
+    st.mark(6);
+    if constexpr (REGEN) {
+      // ---- 3'. regenerate: the recovered point e_w IS replica e_w's cells
+      // (P(e_w) stripe by stripe).  Undo the stage-1 transpose and store it as
+      // big-endian cells, one 1 KiB store per wave-instruction; no
+      // interpolation (fused "decode + re-encode" of sync_process.cpp:313-335).
+      // (RT: row w's slot K + w, for w < the tile's rows)
+      if constexpr (RT) prefetch(tile + t_step);
+      if constexpr (BATCH) {
+        if (RT ? (uint32_t)wave < rt_rows : wave < S::kM) {
+          uint32_t Pl[16], W[16];
+          syn_get_point(L, my_erased, Pl);
+#pragma unroll
+          for (int b = 0; b < 16; ++b) W[b ^ 8] = Pl[b];
+          transpose16x2(W, bm);  // self-inverse: back to the loaded word layout
+          const uint32_t trailer = s_ld(&a.tiles[tile].trailer);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const SynBatchObj &d = half_obj(tile, h);
+            uint8_t *const rg = s_ld(&d.regen[wave]);
+            if (rg == nullptr) continue;
+            const uint64_t st0 = half_s0(tile, h);
+            const uint64_t clen = s_ld(&d.chunk_len);
+            // the T cells; the trailer cell is copied from survivor 0 by the
+            // object's last half (as restore + re-encode writes it)
+            const int64_t valid = (int64_t)clen - 2 - (int64_t)(2 * st0);
+            uint8_t *dst = rg + 2 * st0 + 16 * lane;
+            if (valid >= 2 * (int64_t)kHalfStripes) {
+#pragma unroll
+              for (int q = 0; q < 2; ++q)
+                g_st<8>(dst + 1024 * q, u32x4{W[8 * h + 4 * q], W[8 * h + 4 * q + 1], W[8 * h + 4 * q + 2],
+                                              W[8 * h + 4 * q + 3]});
+            } else {
+#pragma unroll
+              for (int q = 0; q < 2; ++q)
+                st16_guard(dst + 1024 * q,
+                           u32x4{W[8 * h + 4 * q], W[8 * h + 4 * q + 1], W[8 * h + 4 * q + 2], W[8 * h + 4 * q + 3]},
+                           valid - 16 * lane - 1024 * q);
+            }
+            if (((trailer >> h) & 1u) && lane == 0)
+              *(gmem<uint16_t> *)(rg + clen - 2) = *(const gmem<uint16_t> *)(s_ld(&d.chunks[0]) + clen - 2);
+          }
+        }
+        __syncthreads();  // every wave is done with this tile's planes
+        continue;
+      }
+      uint8_t *const rg = wave < S::kM ? a.regen[wave] : nullptr;
+      if (rg != nullptr) {
+        uint32_t Pl[16], W[16];
+        syn_get_point(L, my_erased, Pl);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) W[b ^ 8] = Pl[b];
+        transpose16x2(W, bm);  // self-inverse: back to the loaded word layout
+        {
+          uint8_t *dst = rg + (uint64_t)o * a.regen_stride + 2 * stripe0 + 16 * lane;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            g_st<8>(dst + 1024 * q, u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]});
+        }
+      }
+      __syncthreads();  // every wave is done with this tile's planes
+      continue;
+    }
+    // ---- 3. fixed interpolation from points 0..K-1, then big-endian stores
+    {
+      uint32_t cells[16 * S::kCells];
+      syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
+      if (kLateLoad && !BATCH) prefetch(tile + t_step);
+      // this wave's copy-out: 1024 kChunks bytes at wofs of the tile's output
+      // (batch: of its half's object's output, with out_valid bytes of the
+      // object still to go from there)
+      constexpr int kChunks = 4 * K / WV;  // 1 KiB pieces of the tile (2048 stripes x 2K bytes) each wave writes
+      constexpr uint32_t kHalfBytes = kHalfStripes * 2 * K;
+      static_assert(kHalfBytes % (1024u * kChunks) == 0, "a wave's copy-out lies in one half");
+      // (computed where the stores start: live across the staging, the
+      // addresses cost k = 32 SGPR spills)
+      struct Target {
+        uint8_t *g0;
+        int64_t valid;
+        bool guard;
+      };
+      auto target = [&]() -> Target {
+        const uint32_t wofs = 1024u * kChunks * wave;
+        if constexpr (BATCH) {
+          const int h = (int)(wofs / kHalfBytes);
+          const SynBatchObj &d = half_obj(tile, h);
+          const uint64_t at = half_s0(tile, h) * (2 * K) + (wofs - h * kHalfBytes);
+          const int64_t valid = (int64_t)s_ld(&d.out_len) - (int64_t)at;
+          return {s_ld(&d.out) + at + 16u * lane, valid, valid < 1024 * kChunks};
+        } else {
+          return {a.out + (uint64_t)o * a.out_stride + stripe0 * (2 * K) + wofs + 16u * lane,
+                  kNoBound, false};
+        }
+      };
+      constexpr int kGroups = S::kCells / 2;  // word groups (2 cells) per wave
+      if constexpr (K == 16) {
+        // Stage the tile's output in LDS (the planes are dead once every wave
+        // has interpolated), stripe-major with 8 bytes of padding after every
+        // 8 stripes: stripe st at byte 32 st + 8 (st / 8).  Each lane writes
+        // its wave's 8 bytes (cells 4w..4w+3) of a stripe with one
+        // ds_write_b64; lane l's stripes 8 l + e are 264 bytes apart, so the
+        // 16 lanes of a write group cover all 32 banks once (16-byte padding
+        // after every 16 stripes put 4 lanes on each bank of a ds_write_b32:
+        // 4-way conflicts).  The copy-out reads 16 contiguous bytes per lane
+        // as two 8-byte halves, so every HBM write is a whole 1 KiB
+        // wave-instruction (no partial lines).
+        static_assert(S::kCells == 4, "one ds_write_b64 = the wave's 4 cells of a stripe");
+        static_assert(2048 * 32 + 256 * 8 <= S::kLdsBytes, "staging layout is for 32-byte stripes");
+        syn_prio<2, kPrio>();
+        uint32_t rows[2][32];
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int jb = 0; jb < 16; ++jb) rows[g][16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
+          transpose32(rows[g], bm);
+        }
+        __syncthreads();
+        st.mark(14);
+        // slot 8q+e is stripe 8 lane + 512 q + e at byte 264 lane + 16896 q +
+        // 32 e: a per-lane base plus a compile-time offset
+        lds_char *w0 = L.base + 264u * lane + 8u * wave;
+#pragma unroll
+        for (int slot = 0; slot < 32; ++slot) {
+          const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+          *(__attribute__((address_space(3))) u32x2 *)(w0 + (slot >> 3) * 16896 + (slot & 7) * 32) =
+              u32x2{rows[0][pi], rows[1][pi]};
+        }
+        syn_prio<0, kPrio>();
+        st.mark(15);
+        if (BATCH) prefetch(tile + t_step);  // (batch: the staged rows are dead; room for the survivors)
+        __syncthreads();
+        st.mark(16);
+        // 16-byte chunk c = 64 (kChunks wave + i) + lane of the tile: stripe c/2,
+        // half c%2, at 16 c + 8 (c / 16) = r0 + 1056 i
+        const lds_char *r0 = L.base + 1056u * kChunks * wave + 16u * lane + 8u * (lane >> 4);
+        const auto [g0, out_valid, guard] = target();
+        auto piece = [&](int i) {
+          const lds_char *r = r0 + 1056 * i;
+          const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
+          const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
+          return u32x4{v0[0], v0[1], v1[0], v1[1]};
+        };
+        if (!guard) {
+#pragma unroll
+          for (int i = 0; i < kChunks; ++i) g_st<8>(g0 + 1024 * i, piece(i));
+        } else {
+#pragma unroll
+          for (int i = 0; i < kChunks; ++i) st16_guard(g0 + 1024 * i, piece(i), out_valid - 16 * lane - 1024 * i);
+        }
+        st.mark(17);
+      } else {
+        // k = 32: stage as for k = 16 with 64-byte stripes and 8 bytes of
+        // padding after every 8 stripes: stripe st, word w at st*64 + (st/8)*8
+        // + 4w; the copy-out reads 16 bytes per lane as two 8-byte halves.
+        static_assert(K == 32 && S::kCells == 4 && 2048 * 64 + 256 * 8 <= S::kLdsBytes,
+                      "staging layout is for 64-byte stripes");
+        __syncthreads();
+        st.mark(14);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          uint32_t rows[32];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int jb = 0; jb < 16; ++jb) rows[16 * h + jb] = cells[16 * (2 * g + h) + (jb ^ 8)];
+          transpose32(rows, bm);
+          // slot 8q+e is stripe st = 8 lane + 512 q + e: byte 512 lane + 8 lane
+          // + q (32768 + 512) + 64 e + 4 (2 wave + g); lanes l and l + 16 of a
+          // 32-lane group share a bank (one word group at a time keeps 32,
+          // not 64, transposed rows live)
+          lds_char *w0 = L.base + 520u * lane + 4u * (2 * wave + g);
+#pragma unroll
+          for (int slot = 0; slot < 32; ++slot) {
+            const int pi = (slot & 1) ? 16 + (slot >> 1) : (slot >> 1);
+            *(__attribute__((address_space(3))) uint32_t *)(w0 + (slot >> 3) * (32768 + 512) + (slot & 7) * 64) =
+                rows[pi];
+          }
+        }
+        st.mark(15);
+        if (BATCH) prefetch(tile + t_step);  // (batch: the staged rows are dead; room for the survivors)
+        __syncthreads();
+        st.mark(16);
+        // 16-byte chunk c = 64 (16 wave + i) + lane of the tile: stripe c/4,
+        // quarter c%4, at 64 (c/4) + 8 (c/32) + 16 (c%4) = r0 + 1040 i (one
+        // per-lane base, compile-time offsets: no hoisted address per i)
+        static_assert(kChunks == 16, "16 KiB of copy-out per wave");
+        const lds_char *r0 = L.base + 16640u * wave + 64u * (lane >> 2) + 8u * (lane >> 5) + 16u * (lane & 3);
+        const auto [g0, out_valid, guard] = target();
+        auto piece = [&](int i) {
+          const lds_char *r = r0 + 1040 * i;
+          const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
+          const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
+          return u32x4{v0[0], v0[1], v1[0], v1[1]};
+        };
+        if (!guard) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) g_st<8>(g0 + 1024 * i, piece(i));
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) st16_guard(g0 + 1024 * i, piece(i), out_valid - 16 * lane - 1024 * i);
+        }
+        st.mark(17);
+      }
+    }
+    __syncthreads();
+    st.mark(18);
+  }
+  st.flush(blockIdx.x * WV + wave, lane);
+}
+
+}  // namespace vds_ec

@@ -516,7 +516,9 @@ int restore_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint16_
     sa.out_stride = out_stride;
     sa.tiles_per_obj = (uint32_t)plan.tiles;
     sa.total_tiles = (uint32_t)(plan.tiles * count);
-    hipError_t e = launch_restore_syn(k, plan.syn_n, sa, s);
+    // the survivor set's own kernel once it is compiled (vds_ec_jit.cpp)
+    const hipFunction_t jf = jit_restore_function(k, plan.syn_n, sa);
+    hipError_t e = jf ? launch_restore_syn_jit(jf, k, plan.syn_n, sa, s) : launch_restore_syn(k, plan.syn_n, sa, s);
     if (e != hipSuccess) return hip_status(e);
     per_obj = plan.tiles * kTileStripes;
   } else if (plan.path == 2) {
@@ -2642,7 +2644,8 @@ int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size
   bool ok = true;
   const uint64_t len = restored_len(2, k, chunk_size, padding, 0, &ok);
   if (!ok || k == 0) return 1;
-  return plan_restore(2, k, nodes, len, count, 0).path;
+  const int path = plan_restore(2, k, nodes, len, count, 0).path;
+  return path == 3 && jit_enabled() && vds_ec_jit_ready16(k, nodes) ? 4 : path;
 }
 
 }  // extern "C"

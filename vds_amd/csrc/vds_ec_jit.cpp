@@ -1,0 +1,391 @@
+// vds_ec_jit.cpp -- pattern-specific restore kernels compiled at run time.
+//
+// k_restore_syn (ec_restore_syn.hip) serves every survivor set of a compiled
+// (k, n) with fixed syndrome programs plus a runtime M x M recovery walk
+// (chunk_restore<uint16_t>::restore, chunk.h:290-444).  A repair pass meets
+// few survivor sets -- the bench and a node-loss repair meet one -- so for a
+// set seen on a non-batch restore this module generates the straight-line
+// XOR programs of that set (xorprog.hpp: the value at each erased point below
+// k as the Lagrange combination of the survivors, Paar-reduced) and compiles
+// the same kernel body with them (hiprtc in the helper process vds_ec_jitc,
+// gfx950), in place of the syndromes,
+// the recovery walk and its LDS atomics.  Same bytes: the Lagrange
+// combination is the unique polynomial through the survivors, as V_S^{-1} is.
+//
+// Compiles run on one background thread; until a set's kernel is loaded the
+// restore keeps using k_restore_syn.  VDS_EC_JIT=0 disables the module,
+// VDS_EC_JIT=sync compiles on the calling thread at the first use.  The kernel
+// source includes the device headers and the generated interpolation programs,
+// embedded in the helper compiler vds_ec_jitc at build time (vds_amd/build.py).
+#include <dlfcn.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <spawn.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cerrno>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <tuple>
+#include <vector>
+
+#include "ec_internal.hpp"
+#include "vds_ec.h"
+#include "xorprog.hpp"
+
+extern char **environ;
+
+namespace vds_ec {
+namespace {
+
+
+constexpr int kJitMaxDev = 64;
+constexpr size_t kJitMaxEntries = 256;  // distinct survivor sets kept (never evicted: kernels may be in flight)
+constexpr int kFillBlock = 2;           // points per Paar block (k = 16: no spills; 4 spilled 91 VGPRs)
+
+// JIT policy: 0 = off, 1 = background compile from a set's second use
+// (default), 2 = compile on the calling thread at the first use.  Initially
+// from VDS_EC_JIT (0 / off, sync), then vds_ec_jit_set_mode.
+std::atomic<int> &jit_mode_ref() {
+  static std::atomic<int> m{[] {
+    const char *v = std::getenv("VDS_EC_JIT");
+    if (!v) return 1;
+    if (!std::strcmp(v, "0") || !std::strcmp(v, "off")) return 0;
+    if (!std::strcmp(v, "sync")) return 2;
+    return 1;
+  }()};
+  return m;
+}
+int jit_mode() { return jit_mode_ref().load(std::memory_order_relaxed); }
+constexpr int kJitSightings = 2;         // async mode: uses of a set before its compile is queued
+constexpr size_t kJitMaxSeen = 1 << 14;  // sighting counts kept (cleared when full)
+
+struct Key {
+  uint32_t k, n;
+  uint64_t survivors;  // bit a: point a survives
+  bool operator<(const Key &o) const { return std::tie(k, n, survivors) < std::tie(o.k, o.n, o.survivors); }
+};
+
+struct Entry {
+  enum State { kPending, kReady, kFailed };
+  State state = kPending;
+  std::vector<char> code;
+  std::string log;
+  hipModule_t mod[kJitMaxDev] = {};
+  hipFunction_t fn[kJitMaxDev] = {};
+};
+
+// The kernel source for one survivor set.
+std::string kernel_source(const Key &key) {
+  const int K = (int)key.k, N = (int)key.n, WV = K / 4;
+  std::vector<int> sp;
+  for (int a = 0; a < N; ++a)
+    if ((key.survivors >> a) & 1u) sp.push_back(a);
+  std::string s;
+  xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
+  xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
+  xorgen::emit_fill_programs(s, "JitFill", K, sp, kFillBlock);
+  xorgen::appendf(s, "}  // namespace vds_ec\n");
+  xorgen::appendf(s,
+                  "extern \"C\" __global__ __launch_bounds__((vds_ec::SynShape<%d, %d, %d>::kThreads), "
+                  "(vds_ec::SynShape<%d, %d, %d>::kWavesPerSimd))\n"
+                  "void vds_ec_jit_restore(vds_ec::SynRestoreArgs a) {\n"
+                  "  vds_ec::restore_syn_body<%d, %d, %d, false, false, false, vds_ec::JitFill>(a);\n}\n",
+                  K, N, WV, K, N, WV, K, N, WV);
+  return s;
+}
+
+// The helper compiler next to this library (vds_ec_jitc.cpp says why it is a
+// separate process).
+std::string helper_path() {
+  Dl_info info{};
+  if (!dladdr(reinterpret_cast<void *>(&helper_path), &info) || !info.dli_fname) return {};
+  std::string p = info.dli_fname;
+  const size_t slash = p.rfind('/');
+  return (slash == std::string::npos ? std::string(".") : p.substr(0, slash)) + "/vds_ec_jitc";
+}
+
+std::string read_file(const std::string &path) {
+  std::string out;
+  if (FILE *f = std::fopen(path.c_str(), "rb")) {
+    char buf[65536];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) out.append(buf, n);
+    std::fclose(f);
+  }
+  return out;
+}
+
+// Compile one survivor set's kernel with the helper (host only: no device
+// needed): source and code object pass through a private temporary directory.
+bool compile(const Key &key, std::vector<char> &code, std::string &log) {
+  const std::string src = kernel_source(key);
+  const std::string helper = helper_path();
+  if (helper.empty() || access(helper.c_str(), X_OK) != 0) {
+    log = "vds_ec_jitc not found next to libvds_ec.so";
+    return false;
+  }
+  const char *tmpenv = std::getenv("TMPDIR");
+  std::string dir = std::string(tmpenv && *tmpenv ? tmpenv : "/tmp") + "/vds_ec_jit_XXXXXX";
+  if (!mkdtemp(&dir[0])) {
+    log = "mkdtemp failed";
+    return false;
+  }
+  const std::string in = dir + "/k.hip", out = dir + "/k.co", err = dir + "/log.txt";
+  bool ok = false;
+  if (FILE *f = std::fopen(in.c_str(), "w")) {
+    ok = std::fwrite(src.data(), 1, src.size(), f) == src.size();
+    ok = (std::fclose(f) == 0) && ok;
+  }
+  if (ok) {
+    // a child process (posix_spawn), stderr into the log file
+    posix_spawn_file_actions_t fa;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_addopen(&fa, 2, err.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
+    std::vector<char *> argv = {const_cast<char *>(helper.c_str()), const_cast<char *>(in.c_str()),
+                                const_cast<char *>(out.c_str()), nullptr};
+    pid_t pid = 0;
+    ok = posix_spawn(&pid, helper.c_str(), &fa, nullptr, argv.data(), environ) == 0;
+    posix_spawn_file_actions_destroy(&fa);
+    int status = 0;
+    if (ok) {
+      while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+      }
+      ok = WIFEXITED(status) && WEXITSTATUS(status) == 0;
+    }
+    log = read_file(err);
+    if (ok) {
+      const std::string bytes = read_file(out);
+      code.assign(bytes.begin(), bytes.end());
+      ok = !code.empty();
+    }
+  }
+  // VDS_EC_JIT_DUMP=<dir>: keep the source and code object (inspection)
+  if (const char *dump = std::getenv("VDS_EC_JIT_DUMP")) {
+    char base[512];
+    std::snprintf(base, sizeof base, "%s/jit_%u_%u_%llx", dump, key.k, key.n, (unsigned long long)key.survivors);
+    if (FILE *f = std::fopen((std::string(base) + ".hip").c_str(), "w")) {
+      std::fwrite(src.data(), 1, src.size(), f);
+      std::fclose(f);
+    }
+    if (ok)
+      if (FILE *f = std::fopen((std::string(base) + ".co").c_str(), "wb")) {
+        std::fwrite(code.data(), 1, code.size(), f);
+        std::fclose(f);
+      }
+  }
+  std::remove(in.c_str());
+  std::remove(out.c_str());
+  std::remove(err.c_str());
+  rmdir(dir.c_str());
+  return ok;
+}
+
+class Jit {
+ public:
+  static Jit &get() {
+    static Jit j;
+    return j;
+  }
+
+  // The loaded kernel of `key` on the current device, or nullptr (not
+  // compiled yet -- then queued -- or failed).
+  hipFunction_t function(const Key &key) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kJitMaxDev) return nullptr;
+    std::shared_ptr<Entry> e;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      auto it = map_.find(key);
+      if (it == map_.end()) {
+        if (map_.size() >= kJitMaxEntries) return nullptr;
+        const bool sync = jit_mode() == 2;
+        if (!sync) {  // one-off sets are not worth a compile
+          if (seen_.size() >= kJitMaxSeen) seen_.clear();
+          if (++seen_[key] < kJitSightings) return nullptr;
+          seen_.erase(key);
+        }
+        e = std::make_shared<Entry>();
+        map_.emplace(key, e);
+        if (sync) {
+          lk.unlock();
+          run(key, e);
+          lk.lock();
+        } else {
+          queue_.push_back(key);
+          start_worker();
+          cv_.notify_all();
+          return nullptr;
+        }
+      } else {
+        e = it->second;
+      }
+      if (e->state != Entry::kReady) return nullptr;
+      if (e->fn[dev]) return e->fn[dev];
+    }
+    // first use on this device: load the code object (once per device)
+    std::lock_guard<std::mutex> g(load_mu_);
+    if (!e->fn[dev]) {
+      hipModule_t m = nullptr;
+      hipFunction_t f = nullptr;
+      if (hipModuleLoadData(&m, e->code.data()) != hipSuccess) return nullptr;
+      if (hipModuleGetFunction(&f, m, "vds_ec_jit_restore") != hipSuccess) {
+        (void)hipModuleUnload(m);
+        return nullptr;
+      }
+      e->mod[dev] = m;
+      e->fn[dev] = f;
+    }
+    return e->fn[dev];
+  }
+
+  bool ready(const Key &key) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = map_.find(key);
+    return it != map_.end() && it->second->state == Entry::kReady;
+  }
+
+  // Wait until no compile is queued or running.
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    idle_cv_.wait(lk, [&] { return queue_.empty() && busy_ == 0; });
+  }
+
+  // Compile-only (no device): the code object size of `key`'s kernel.
+  bool build(const Key &key, size_t *bytes, std::string *log) {
+    std::vector<char> code;
+    std::string l;
+    const bool ok = compile(key, code, l);
+    if (bytes) *bytes = ok ? code.size() : 0;
+    if (log) *log = l;
+    return ok;
+  }
+
+  ~Jit() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      queue_.clear();
+    }
+    cv_.notify_all();
+    if (worker_.joinable()) worker_.join();
+  }
+
+ private:
+  void run(const Key &key, const std::shared_ptr<Entry> &e) {
+    std::vector<char> code;
+    std::string log;
+    const bool ok = compile(key, code, log);
+    std::lock_guard<std::mutex> lk(mu_);
+    e->code.swap(code);
+    e->log.swap(log);
+    e->state = ok ? Entry::kReady : Entry::kFailed;
+  }
+
+  void start_worker() {  // (mu_ held)
+    if (worker_.joinable()) return;
+    worker_ = std::thread([this] {
+      std::unique_lock<std::mutex> lk(mu_);
+      while (true) {
+        cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+        if (stop_) break;
+        const Key key = queue_.front();
+        queue_.pop_front();
+        std::shared_ptr<Entry> e = map_[key];
+        ++busy_;
+        lk.unlock();
+        run(key, e);
+        lk.lock();
+        --busy_;
+        if (queue_.empty() && busy_ == 0) idle_cv_.notify_all();
+      }
+      idle_cv_.notify_all();
+    });
+  }
+
+  std::mutex mu_, load_mu_;
+  std::condition_variable cv_, idle_cv_;
+  std::map<Key, std::shared_ptr<Entry>> map_;
+  std::map<Key, int> seen_;
+  std::deque<Key> queue_;
+  std::thread worker_;
+  int busy_ = 0;
+  bool stop_ = false;
+};
+
+Key key_of(uint32_t k, uint32_t n, const uint8_t *points) {
+  Key key{k, n, 0};
+  for (uint32_t j = 0; j < k; ++j) key.survivors |= 1ull << points[j];
+  return key;
+}
+
+}  // namespace
+
+bool jit_enabled() { return jit_mode() != 0; }
+
+hipFunction_t jit_restore_function(uint32_t k, uint32_t n, const SynRestoreArgs &a) {
+  if (jit_mode() == 0 || !has_restore_syn(k, n)) return nullptr;
+  return Jit::get().function(key_of(k, n, a.point));
+}
+
+}  // namespace vds_ec
+
+using namespace vds_ec;
+
+extern "C" {
+
+int vds_ec_jit_set_mode(int mode) {
+  if (mode < 0 || mode > 2) return VDS_EC_EINVAL;
+  jit_mode_ref().store(mode, std::memory_order_relaxed);
+  return VDS_EC_OK;
+}
+
+int vds_ec_jit_wait(void) {
+  Jit::get().wait();
+  return VDS_EC_OK;
+}
+
+// Survivors as replica ids; EINVAL unless they are k distinct points of
+// 0..k+k/4-1 for a compiled (k, k + k/4).
+static int jit_key(uint16_t k, const uint16_t *nodes, Key *key) {
+  const uint32_t n = k + k / 4u;
+  if (!nodes || k == 0 || k % 4 || !has_restore_syn(k, n)) return VDS_EC_EINVAL;
+  *key = Key{k, n, 0};
+  for (uint32_t j = 0; j < k; ++j) {
+    if (nodes[j] >= n || ((key->survivors >> nodes[j]) & 1u)) return VDS_EC_EINVAL;
+    key->survivors |= 1ull << nodes[j];
+  }
+  return VDS_EC_OK;
+}
+
+int vds_ec_jit_build16(uint16_t k, const uint16_t *nodes, uint64_t *code_bytes) {
+  Key key;
+  const int rc = jit_key(k, nodes, &key);
+  if (rc) return rc;
+  size_t bytes = 0;
+  std::string log;
+  if (!Jit::get().build(key, &bytes, &log)) {
+    std::fprintf(stderr, "vds_ec jit: compile failed:\n%s\n", log.c_str());
+    return VDS_EC_EHIP;
+  }
+  if (code_bytes) *code_bytes = bytes;
+  return VDS_EC_OK;
+}
+
+int vds_ec_jit_ready16(uint16_t k, const uint16_t *nodes) {
+  Key key;
+  if (jit_key(k, nodes, &key)) return 0;
+  return Jit::get().ready(key) ? 1 : 0;
+}
+
+}  // extern "C"

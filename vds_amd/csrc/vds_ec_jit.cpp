@@ -51,7 +51,24 @@ namespace {
 
 constexpr int kJitMaxDev = 64;
 constexpr size_t kJitMaxEntries = 256;  // distinct survivor sets kept (never evicted: kernels may be in flight)
-constexpr int kFillBlock = 2;           // points per Paar block (k = 16: no spills; 4 spilled 91 VGPRs)
+// Points per Paar block of the fill programs, and whether a block's LDS reads
+// are issued before the previous block's XORs.  k = 16, no spills up to 3
+// with prefetch (4 spilled 91 VGPRs) and 4 without; same-box repair, 512 x
+// 64 MiB: 2 14.62-14.72 ms, 3 14.52-14.60, 4 without prefetch 14.62
+// (profiles/round3/ab/jit_knobs.log).  VDS_EC_JIT_PB / VDS_EC_JIT_NOPF
+// override them (A/B).
+int fill_block() {
+  static const int pb = [] {
+    const char *v = std::getenv("VDS_EC_JIT_PB");
+    const int x = v ? std::atoi(v) : 0;
+    return x > 0 && x <= 32 ? x : 3;
+  }();
+  return pb;
+}
+bool fill_prefetch() {
+  static const bool pf = std::getenv("VDS_EC_JIT_NOPF") == nullptr;
+  return pf;
+}
 
 // JIT policy: 0 = off, 1 = background compile from a set's second use
 // (default), 2 = compile on the calling thread at the first use.  Initially
@@ -94,7 +111,7 @@ std::string kernel_source(const Key &key) {
   std::string s;
   xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
   xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
-  xorgen::emit_fill_programs(s, "JitFill", K, sp, kFillBlock);
+  xorgen::emit_fill_programs(s, "JitFill", K, sp, fill_block(), fill_prefetch());
   xorgen::appendf(s, "}  // namespace vds_ec\n");
   xorgen::appendf(s,
                   "extern \"C\" __global__ __launch_bounds__((vds_ec::SynShape<%d, %d, %d>::kThreads), "

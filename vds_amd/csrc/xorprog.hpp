@@ -284,7 +284,7 @@ inline size_t emit_compute(std::string &s, const Block &B, int bi, bool first) {
 // blocked by `pb`.  The LDS reads of block b + 1 are issued before the XORs of
 // block b so their latency hides under them.  Returns the instruction count.
 inline size_t emit_program(std::string &s, const char *name, const std::vector<std::vector<int>> &rows, int C,
-                           const std::vector<int> &rowsel, int pb, const InputMap &im) {
+                           const std::vector<int> &rowsel, int pb, const InputMap &im, bool prefetch = true) {
   const int nrows = (int)rowsel.size();
   appendf(s, "  template <typename In>\n  __device__ __forceinline__ static void %s(const In &IN4, uint32_t (&acc)[%d]) {\n",
           name, nrows);
@@ -300,7 +300,8 @@ inline size_t emit_program(std::string &s, const char *name, const std::vector<s
   size_t ops = 0;
   emit_loads(s, blocks[0], 0, im);
   for (size_t b = 0; b < blocks.size(); ++b) {
-    if (b + 1 < blocks.size()) emit_loads(s, blocks[b + 1], (int)b + 1, im);
+    if (b > 0 && !prefetch) emit_loads(s, blocks[b], (int)b, im);
+    if (b + 1 < blocks.size() && prefetch) emit_loads(s, blocks[b + 1], (int)b + 1, im);
     ops += emit_compute(s, blocks[b], (int)b, b == 0);
     // keep the scheduler from hoisting later blocks' LDS reads (and their
     // registers) above this block
@@ -324,7 +325,8 @@ inline std::vector<int> row_range(int row0, int n) {
 // reference's V_S^{-1} route (chunk.h:290-444) for every input.  Survivor j is
 // read from its own LDS slot spoints[j].  Emits `struct NAME { kFill, kPoint,
 // fill0.., fill(w, IN4, acc) }`; returns the instruction count.
-inline size_t emit_fill_programs(std::string &s, const char *name, int K, const std::vector<int> &spoints, int pb) {
+inline size_t emit_fill_programs(std::string &s, const char *name, int K, const std::vector<int> &spoints, int pb,
+                                 bool prefetch = true) {
   std::vector<int> EU;
   for (int a = 0; a < K; ++a)
     if (std::find(spoints.begin(), spoints.end(), a) == spoints.end()) EU.push_back(a);
@@ -350,7 +352,7 @@ inline size_t emit_fill_programs(std::string &s, const char *name, int K, const 
   for (size_t m = 0; m < EU.size(); ++m) {
     char nm[32];
     std::snprintf(nm, sizeof nm, "fill%zu", m);
-    total += emit_program(s, nm, rows, K, row_range(16 * (int)m, 16), pb, im);
+    total += emit_program(s, nm, rows, K, row_range(16 * (int)m, 16), pb, im, prefetch);
   }
   appendf(s, "  template <typename In>\n  __device__ __forceinline__ static void fill(int w, const In &IN4, uint32_t (&acc)[16]) {\n");
   appendf(s, "    switch (w) {\n");

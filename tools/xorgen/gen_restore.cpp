@@ -45,6 +45,155 @@ static size_t emit_program(const char *name, const std::vector<std::vector<int>>
   return ops;
 }
 
+// ------------------------------------------------------------------
+// Two-level additive-FFT interpolation from the points 0..K-1 (K = 2^m; wave
+// W owns slots 4W..4W+3), k_restore_syn's gm2 stages:
+//   S1 (local to wave W's four slots): level 1, the pairs (2i, 2i+1) of U =
+//      span{1, x, ..}: q1_i = v_2i + v_2i+1 -> slot 2i+1, q0_i = v_2i + 2i q1_i
+//      -> slot 2i; P(X) = P0(X^2+X) + X P1(X^2+X), P0 / P1 take q0 / q1 on D =
+//      s(2i) (index i <-> sum_t bit_t(i) d_t, d_t = s(x^(t+1)), s = X^2+X).
+//      Level 2 on Q_par (par 0: P0, 1: P1), normalised by delta = d_0 (R(Y) =
+//      Q(delta Y) on the points ptR(h) = sum_t bit_t(h) d_t / delta, which
+//      contain 1): the pairs (2j, 2j+1): r1_j = v + v', r0_j = v + ptR(2j) r1_j
+//      -> slots 4j + par (r0) and 4j + 2 + par (r1).  Both levels touch only
+//      slots 4W..4W+3 (j = W, i = 2W, 2W+1).
+//   S2: family f (slots 4j + f: f = par for R0 of Q_par, par + 2 for R1) is
+//      interpolated directly on its K/4 points s(ptR(2j)); coefficient c ->
+//      slot 4c + f.  K = 16: one wave per family, in place; K = 32: two.
+//   S3: Q_par coefficient i = delta^-i (sum_c [C(c, i-c) odd] R0_c + [C(c,
+//      i-1-c) odd] R1_c) (the expansion R(Y) = R0(Y^2+Y) + Y R1(Y^2+Y), then
+//      the twist) -> slot (K/2) par + i: the layout stage C reads.
+static bool binom_odd(int n, int r) { return r >= 0 && r <= n && (r & ~n) == 0; }
+
+// acc[0..16) *= c in place (a Paar program on the 16 x 16 bit matrix of c)
+static size_t emit_twist(const char *name, uint32_t c) {
+  std::vector<uint32_t> M = {c};
+  const auto rows = all_bitrows(M, 1, 1);
+  const xorgen::Block B = xorgen::make_block(xorgen::paar(16, rows), 0);
+  std::string s;
+  xorgen::appendf(s, "  __device__ __forceinline__ static void %s(uint32_t (&acc)[16]) {\n", name);
+  for (int g = 0; g < 4; ++g)
+    xorgen::appendf(s, "    const u32x4 g0_%d = {acc[%d], acc[%d], acc[%d], acc[%d]};\n", g, 4 * g, 4 * g + 1, 4 * g + 2,
+                    4 * g + 3);
+  const size_t ops = xorgen::emit_compute(s, B, 0, true);
+  xorgen::appendf(s, "  }\n");
+  std::fputs(s.c_str(), stdout);
+  return ops;
+}
+
+static size_t emit_gm2(int K, int waves) {
+  const int H = K / 2, F = K / 4;  // Q size, family size
+  int m = 0;
+  while ((1 << m) < K) ++m;
+  std::vector<uint32_t> d(m - 1), nb(m - 1);
+  for (int t = 0; t < m - 1; ++t) d[t] = gf16_mul(1u << (t + 1), 1u << (t + 1)) ^ (1u << (t + 1));
+  const uint32_t delta = d[0], dinv = gf16_inv(delta);
+  for (int t = 0; t < m - 1; ++t) nb[t] = gf16_mul(d[t], dinv);
+  auto ptR = [&](int h) {
+    uint32_t p = 0;
+    for (int t = 0; t < m - 1; ++t)
+      if ((h >> t) & 1) p ^= nb[t];
+    return p;
+  };
+  size_t total = 0;
+  std::printf("  // two-level interpolation (gm2; see tools/xorgen/gen_restore.cpp emit_gm2)\n");
+  std::printf("  static constexpr bool kGm2 = true;\n");
+  // S1: wave W, slots 4W..4W+3 -> the same slots
+  for (int w = 0; w < waves; ++w) {
+    std::vector<uint32_t> M(16, 0);  // 4 x 4: out slot 4W+o from in slot 4W+i
+    // level 1 on pairs (4W, 4W+1), (4W+2, 4W+3): q0 -> even, q1 -> odd slot
+    uint32_t L1[4][4] = {};
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t g = 2 * (2 * w + q);
+      L1[2 * q][2 * q] = 1u ^ g, L1[2 * q][2 * q + 1] = g;  // q0 = (1 + g) v0 + g v1
+      L1[2 * q + 1][2 * q] = 1u, L1[2 * q + 1][2 * q + 1] = 1u;
+    }
+    // level 2: for par, v = slot 4W + par (index 2W of Q_par), v' = slot 4W + 2 + par
+    uint32_t L2[4][4] = {};
+    const uint32_t g2 = ptR(2 * w);
+    for (int par = 0; par < 2; ++par) {
+      L2[par][par] = 1u ^ g2, L2[par][par + 2] = g2;
+      L2[par + 2][par] = 1u, L2[par + 2][par + 2] = 1u;
+    }
+    for (int o = 0; o < 4; ++o)
+      for (int i = 0; i < 4; ++i) {
+        uint32_t acc = 0;
+        for (int k = 0; k < 4; ++k) acc ^= gf16_mul(L2[o][k], L1[k][i]);
+        M[o * 4 + i] = acc;
+      }
+    const auto rows = all_bitrows(M, 4, 4);
+    xorgen::InputMap im;
+    for (int i = 0; i < 4; ++i) im.map.push_back(4 * w + i);
+    char name[32];
+    std::snprintf(name, sizeof name, "gm_s1_%d", w);
+    std::string s;
+    total += xorgen::emit_program(s, name, rows, 4, row_range(0, 64), 2, im);
+    std::fputs(s.c_str(), stdout);
+  }
+  // S2: family interpolation on the points s(ptR(2j))
+  std::vector<uint16_t> dp(F), dinvm((size_t)F * F);
+  for (int j = 0; j < F; ++j) {
+    const uint32_t p = ptR(2 * j);
+    dp[j] = (uint16_t)(gf16_mul(p, p) ^ p);
+  }
+  if (vds_ec_inverse16(F, dp.data(), dinvm.data()) != VDS_EC_OK) std::exit(1);
+  const std::vector<uint32_t> M2(dinvm.begin(), dinvm.end());
+  const auto rows2 = all_bitrows(M2, F, F);
+  const int wpf = waves / 4;  // waves per family
+  for (int w = 0; w < waves; ++w) {
+    const int f = w / wpf, c0 = 4 * (w % wpf);
+    xorgen::InputMap im;
+    for (int j = 0; j < F; ++j) im.map.push_back(4 * j + f);
+    std::vector<int> rowsel;
+    for (int c = c0; c < c0 + 4; ++c)
+      for (int b = 0; b < 16; ++b) rowsel.push_back(16 * c + b);
+    char name[32];
+    std::snprintf(name, sizeof name, "gm_s2_%d", w);
+    std::string s;
+    total += xorgen::emit_program(s, name, rows2, F, rowsel, 2, im);
+    std::fputs(s.c_str(), stdout);
+  }
+  // S3: the XOR sums (0/1 map from the K R-coefficient slots), then the twists
+  std::vector<uint32_t> M3((size_t)K * K, 0);  // row (H par + i), column slot
+  for (int par = 0; par < 2; ++par)
+    for (int i = 0; i < H; ++i)
+      for (int c = 0; c < F; ++c) {
+        if (binom_odd(c, i - c)) M3[(size_t)(H * par + i) * K + 4 * c + par] ^= 1u;
+        if (binom_odd(c, i - 1 - c)) M3[(size_t)(H * par + i) * K + 4 * c + par + 2] ^= 1u;
+      }
+  const auto rows3 = all_bitrows(M3, K, K);
+  const int wpq = waves / 2;  // waves per Q
+  for (int w = 0; w < waves; ++w) {
+    const int par = w / wpq, i0 = 4 * (w % wpq);
+    std::vector<int> rowsel;
+    for (int i = i0; i < i0 + 4; ++i)
+      for (int b = 0; b < 16; ++b) rowsel.push_back(16 * (H * par + i) + b);
+    char name[32];
+    std::snprintf(name, sizeof name, "gm_s3sum_%d", w);
+    std::string s;
+    xorgen::InputMap im;
+    total += xorgen::emit_program(s, name, rows3, K, rowsel, 4, im);
+    std::fputs(s.c_str(), stdout);
+  }
+  for (int i = 1; i < H; ++i) {
+    char name[32];
+    std::snprintf(name, sizeof name, "gm_tw%d", i);
+    total += (size_t)2 * emit_twist(name, gf16_pow(dinv, (uint32_t)i));  // (applied to both Q)
+  }
+  // dispatch
+  for (const char *st : {"gm_s1_", "gm_s2_", "gm_s3sum_"}) {
+    std::printf("  template <typename In>\n  __device__ __forceinline__ static void %s(int w, const In &IN4, uint32_t (&acc)[64]) {\n", st);
+    std::printf("    switch (w) {\n");
+    for (int w = 0; w < waves; ++w) std::printf("      case %d: %s%d(IN4, acc); break;\n", w, st, w);
+    std::printf("      default: break;\n    }\n  }\n");
+  }
+  std::printf("  // acc (Q coefficients i0..i0+3) *= delta^-i\n");
+  std::printf("  __device__ __forceinline__ static void gm_twist(int i, uint32_t (&acc)[16]) {\n    switch (i) {\n");
+  for (int i = 1; i < H; ++i) std::printf("      case %d: gm_tw%d(acc); break;\n", i, i);
+  std::printf("      default: break;\n    }\n  }\n");
+  return total;
+}
+
 // Fill programs for one erased set: wave w computes the value at erased point
 // E[w] as the fixed combination of the K survivors (Lagrange over S), reading
 // survivor j from its own LDS slot S[j].
@@ -177,7 +326,9 @@ int main(int argc, char **argv) {
   }
   std::printf("  static constexpr int kXorOps = %zu;\n", total);
   std::printf("  static constexpr int kXorOpsHalf = %zu;  // stage B (all four waves)\n", total_b);
+  const size_t total_gm2 = emit_gm2(K, waves);
   std::printf("};\n");
+  std::fprintf(stderr, "two-level interpolation: %zu XOR instructions per 32 stripes\n", total_gm2);
   std::fprintf(stderr, "K=%d N=%d waves=%d: %zu XOR instructions per 32 stripes (stage B: %zu)\n", K, N, waves, total,
                total_b);
   return 0;

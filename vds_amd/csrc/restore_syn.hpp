@@ -229,6 +229,59 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
   }
 }
 
+// Two-level interpolation (VDS_GM2, default; generated gm_* programs,
+// tools/xorgen/gen_restore.cpp emit_gm2): levels 1 and 2 of the additive FFT
+// on each wave's own four slots (S1, in place), the K/4-point direct
+// interpolation of the four level-2 families (S2), the level-2 expansion and
+// twist (S3, into stage C's layout), then stage C.  Against one level + K/2-
+// point direct programs: 3175 vs ~4700 XOR instructions per tile at k = 16,
+// 12311 vs ~20000 at k = 32, for one (k = 16) or two more barriers.
+#ifndef VDS_GM2
+#define VDS_GM2 1
+#endif
+template <int K, int N, int WV, int W>
+__device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
+  using P = RestorePrograms<K, N, WV>;
+  constexpr bool kPrio = SynShape<K, N, WV>::kPrio;
+  constexpr int H = K / 2, kWpf = WV / 4, kWpq = WV / 2;
+  if constexpr (W < WV) {
+    if (wave != W) return syn_interp_gm2<K, N, WV, W + 1>(wave, L, cells, st);
+    uint32_t acc[64];
+    auto cell = [&](int c) -> uint32_t(&)[16] { return *reinterpret_cast<uint32_t(*)[16]>(acc + 16 * c); };
+    // S1: levels 1 and 2 on this wave's slots 4W..4W+3 (only this wave touches them)
+    syn_prio<1, kPrio>();
+    P::gm_s1_(W, L, acc);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) syn_put_point(L, 4 * W + c, cell(c));
+    syn_prio<0, kPrio>();
+    st.mark(7);
+    __syncthreads();
+    st.mark(8);
+    // S2: family f = W / kWpf (slots 4j + f), coefficients c0.. -> slot 4c + f
+    P::gm_s2_(W, L, acc);
+    constexpr int f = W / kWpf, c0 = 4 * (W % kWpf);
+    if constexpr (kWpf > 1) __syncthreads();  // (every wave of the family has read it)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) syn_put_point(L, 4 * (c0 + c) + f, cell(c));
+    st.mark(9);
+    __syncthreads();
+    st.mark(10);
+    // S3: Q_par coefficients i0.. (expansion sums, then the twists) -> slot H par + i
+    P::gm_s3sum_(W, L, acc);
+    constexpr int par = W / kWpq, i0 = 4 * (W % kWpq);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) P::gm_twist(i0 + c, cell(c));
+    __syncthreads();  // every wave has read the R coefficients
+#pragma unroll
+    for (int c = 0; c < 4; ++c) syn_put_point(L, H * par + i0 + c, cell(c));
+    st.mark(11);
+    __syncthreads();
+    st.mark(12);
+    syn_gm_stage_c<K, W, K / WV>(L, cells);
+    st.mark(13);
+  }
+}
+
 // One coefficient-bit pair of the recovery walk: acc ^= T, T1 or T ^ T1 as
 // the pair's two bits select (two = bit b | bit b+1 << 8), in one asm block
 // with its own branches.  As plain C++ the three arms computed into
@@ -747,7 +800,10 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     // ---- 3. fixed interpolation from points 0..K-1, then big-endian stores
     {
       uint32_t cells[16 * S::kCells];
-      syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
+      if constexpr (VDS_GM2 != 0)
+        syn_interp_gm2<K, N, WV, 0>(wave, L, cells, st);
+      else
+        syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
       if (kLateLoad && !BATCH) prefetch(tile + t_step);
       // this wave's copy-out: 1024 kChunks bytes at wofs of the tile's output
       // (batch: of its half's object's output, with out_valid bytes of the

@@ -45,6 +45,10 @@
 
 extern char **environ;
 
+#ifndef VDS_GM2
+#define VDS_GM2 1  // (restore_syn.hpp's default)
+#endif
+
 namespace vds_ec {
 namespace {
 
@@ -109,6 +113,7 @@ std::string kernel_source(const Key &key) {
   for (int a = 0; a < N; ++a)
     if ((key.survivors >> a) & 1u) sp.push_back(a);
   std::string s;
+  xorgen::appendf(s, "#define VDS_GM2 %d\n", VDS_GM2);  // (the interpolation this library was built with)
   xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
   xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
   xorgen::emit_fill_programs(s, "JitFill", K, sp, fill_block(), fill_prefetch());

@@ -18,11 +18,14 @@ echo "[8/9] k32"; timeout -k 10 240 $P --pmc FETCH_SIZE -d $D/pmc_fetch32 -o run
 timeout -k 10 240 $P --pmc WRITE_SIZE -d $D/pmc_write32 -o run -- python tools/prof_kernels.py --k 32 --m 8 --objects 32 --iters 2 > $D/pmc_write32.log 2>&1 &&
 python tools/pmc_traffic.py $D/pmc_fetch32 $D/pmc_write32 32 $D/traffic_k32.json 32 40 > /dev/null &&
 timeout -k 10 400 python bench.py --k 32 --m 8 --objects 512 --no-cpu-baseline --traffic-json $D/traffic_k32.json > $D/bench_k32.log 2>&1 &&
-echo "[9/9] host"; timeout -k 10 400 python tools/bench_host.py --objects 16 --live 16384 > $D/bench_host.log 2>&1
+echo "[9/9] host"; timeout -k 10 400 python tools/bench_host.py --objects 16 --live 16384 > $D/bench_host.log 2>&1 &&
+echo "[+] pcie duplex / drop-in loop"; timeout -k 10 120 tools/ubench/pcie_duplex 256 > $D/pcie_duplex.json 2>&1 &&
+timeout -k 10 120 tools/dropin_loop 200 > $D/dropin_loop.json 2>&1
 rc=$?
 echo "rc=$rc"
 tail -2 $D/pytest_gpu.log
 tail -1 $D/bench_default.log
 tail -1 $D/bench_k32.log
 tail -1 $D/bench_host.log
+cat $D/pcie_duplex.json $D/dropin_loop.json
 exit $rc

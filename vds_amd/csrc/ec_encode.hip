@@ -89,6 +89,51 @@ constexpr PairPlan<WAVES, PPW> plan_pairs() {
   return p;
 }
 
+// ---- two-level additive split (QUAD).  After the level-1 Taylor step, each
+// half P_H (H = 0, 1; degree < K/2) is normalised by 6 = s(x) (Q_H(Z) =
+// P_H(6Z): coefficient i times 6^i) and Taylor-expanded at Z^2 + Z again:
+// Q_H(Z) = A_H(Z^2+Z) + Z B_H(Z^2+Z), degree < K/4.  For the quad of replicas
+// 4j..4j+3, y0 = s(4j) and y1 = s(4j+2) = y0 + 6 share w = z0^2 + z0 with z0
+// = y0 / 6 (z1 = z0 + 1), so
+//   P_H(y0) = A_H(w) + z0 B_H(w),      P_H(y1) = P_H(y0) + B_H(w),
+//   P(4j) = P0(y0) + 4j P1(y0),        P(4j+1) = P(4j) + P1(y0),
+//   P(4j+2) = P0(y1) + (4j+2) P1(y1),  P(4j+3) = P(4j+2) + P1(y1):
+// four K/4-step Horners with the one constant w per quad, against four
+// K/2-step ones for the same four replicas as two level-1 pairs.
+constexpr uint32_t kQuadD = 6u;  // s(x) = x^2 + x
+constexpr uint32_t quad_z0(int j) { return gf16_mul(pair_y(4 * j), gf16_inv(kQuadD)); }
+constexpr uint32_t quad_w(int j) { return gf16_mul(quad_z0(j), quad_z0(j)) ^ quad_z0(j); }
+constexpr int quad_cost(int j) { return 4 * horner_cost((int)quad_w(j)) + 4; }
+
+template <int WAVES, int QPW>
+struct QuadPlan {
+  int j[WAVES][QPW];  // quad index (replicas 4j..4j+3); -1: empty
+};
+
+template <int N, int WAVES, int QPW>
+constexpr QuadPlan<WAVES, QPW> plan_quads() {
+  QuadPlan<WAVES, QPW> p{};
+  int load[WAVES] = {};
+  int cnt[WAVES] = {};
+  bool used[N / 4 + 1] = {};
+  int cost[N / 4 + 1] = {};
+  for (int q = 0; q < N / 4; ++q) cost[q] = quad_cost(q);
+  for (int w = 0; w < WAVES; ++w)
+    for (int s = 0; s < QPW; ++s) p.j[w][s] = -1;
+  for (int it = 0; it < N / 4; ++it) {
+    int best = -1;
+    for (int q = 0; q < N / 4; ++q)
+      if (!used[q] && (best < 0 || cost[q] > cost[best])) best = q;
+    used[best] = true;
+    int bw = -1;
+    for (int w = 0; w < WAVES; ++w)
+      if (cnt[w] < QPW && (bw < 0 || load[w] < load[bw])) bw = w;
+    p.j[bw][cnt[bw]++] = best;
+    load[bw] += cost[best];
+  }
+  return p;
+}
+
 template <int K, int N, int RPW, int WV>
 struct EncodeShape {
   // Loads: every lane takes two dwords (4 cells) of each of its set's 32
@@ -113,6 +158,8 @@ struct EncodeShape {
   static constexpr ReplicaPlan<N, kWaves, RPW> kPlan = plan_replicas<N, kWaves, RPW>();
   static constexpr int kPPW = (N / 2 + kWaves - 1) / kWaves;  // replica pairs per wave (split mode)
   static constexpr PairPlan<kWaves, kPPW> kPairs = plan_pairs<N, kWaves, kPPW>();
+  static constexpr int kQPW = (N / 4 + kWaves - 1) / kWaves;  // replica quads per wave (quad mode)
+  static constexpr QuadPlan<kWaves, kQPW> kQuads = plan_quads<N, kWaves, kQPW>();
   static_assert(K % 4 == 0 && WV == K / 4, "fast encode: k % 4 == 0 and k/4 waves");
   static_assert(RPW * WV >= N, "every replica needs a wave");
   __device__ __forceinline__ static constexpr int cell_off(int c) { return 16 * c + kGroupPad * (c >> 2); }
@@ -459,6 +506,131 @@ __device__ __forceinline__ void pair_zero_dispatch(int wave, const FastEncodeArg
   }
 }
 
+// ---- quad mode
+
+// Level 2 in LDS, step 1 (cell-parallel: every cm mixes all 16 planes): cell
+// 2i + H *= 6^i for i = 1..K/2-1, cells dealt round-robin over the waves.
+template <int K, int N, int RPW, int WV, int C = 2>
+__device__ __forceinline__ void quad_twist_lds(int wave, uint32_t *set_planes) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  if constexpr (C < K) {
+    if (wave == C % WV) {
+      constexpr uint32_t tw = gf16_pow(kQuadD, (uint32_t)(C / 2));
+      uint32_t *p = set_planes + S::cell_off(C);
+      const Plane16 v = plane_horner_rows<tw>(lds_planes(p), plane_zero());
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        *(lds_v4 *)(p + 4 * m) = u32x4{v.p[4 * m], v.p[4 * m + 1], v.p[4 * m + 2], v.p[4 * m + 3]};
+    }
+    quad_twist_lds<K, N, RPW, WV, C + 1>(wave, set_planes);
+  }
+}
+
+// Level 2 in LDS, step 2 (plane-parallel, XORs only): each half's twisted
+// coefficients (cells 2i + H) Taylor-expanded at Z^2 + Z in place: A_H,u at
+// cell 4u + H, B_H,u at cell 4u + 2 + H.
+template <int K, int N, int RPW, int WV>
+__device__ __forceinline__ void quad_taylor_lds(int wave, uint32_t *set_planes) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  if (wave < 4) {
+#pragma unroll
+    for (int H = 0; H < 2; ++H) {
+      u32x4 c[K / 2];
+#pragma unroll
+      for (int i = 0; i < K / 2; ++i) c[i] = *(lds_u32x4 *)(set_planes + S::cell_off(2 * i + H) + 4 * wave);
+      taylor_inplace<K / 2, 0, K / 2>(c);
+#pragma unroll
+      for (int i = 0; i < K / 2; ++i) *(lds_v4 *)(set_planes + S::cell_off(2 * i + H) + 4 * wave) = c[i];
+    }
+  }
+}
+
+// acc = sum_u coef(cell 4u + OFF) w^u by Horner, two steps per iteration.
+// (The two chains A_H, B_H interleaved in one loop spill 18-32 VGPRs at k = 32
+// beside the prefetched tile.)
+template <int K, int N, int RPW, int WV, uint32_t W, int OFF>
+__device__ __forceinline__ Plane16 quad_horner(const uint32_t *set_planes) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  constexpr int Q = K / 4;
+  auto X = [&](int u) { return lds_planes(set_planes + S::cell_off(4 * u + OFF)); };
+  Plane16 A = X(Q - 1), B;
+  Plane16 xa = X(Q - 2);
+#pragma clang loop unroll(disable)
+  for (int u = Q - 2; u >= 1; u -= 2) {
+    const Plane16 xb = X(u - 1);
+    B = plane_horner_rows<W>(A, xa);
+    xa = X(u - 2);
+    A = plane_horner_rows<W>(B, xb);
+  }
+  return plane_horner_rows<W>(A, xa);
+}
+
+template <int K, int N, int RPW, int WV, int W, bool ST, int S0 = 0>
+__device__ __forceinline__ void encode_quad_group(const uint32_t *set_planes, const FastEncodeArgs &a, TilePos tp,
+                                                  int lane, const BitMasks &bm) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  if constexpr (S0 < S::kQPW) {
+    constexpr int j = S::kQuads.j[W][S0];
+    if constexpr (j >= 0) {
+      constexpr uint32_t w = quad_w(j), z0 = quad_z0(j);
+      // P_H(y0), P_H(y1) for H = 0, 1 (H = 1 first: its values are scaled below)
+      Plane16 p1y0, p1y1;
+      {
+        const Plane16 A1 = quad_horner<K, N, RPW, WV, w, 1>(set_planes);
+        const Plane16 B1 = quad_horner<K, N, RPW, WV, w, 3>(set_planes);
+        p1y0 = plane_horner_rows<z0>(B1, A1);
+        p1y1 = plane_xor(p1y0, B1);
+      }
+      const Plane16 A0 = quad_horner<K, N, RPW, WV, w, 0>(set_planes);
+      const Plane16 B0 = quad_horner<K, N, RPW, WV, w, 2>(set_planes);
+      const Plane16 p0y0 = plane_horner_rows<z0>(B0, A0);
+      const Plane16 p0y1 = plane_xor(p0y0, B0);
+      __builtin_amdgcn_s_setprio(kEncStorePrio);
+      const Plane16 r0 = plane_horner_rows<(uint32_t)(4 * j)>(p1y0, p0y0);
+      store_rep<S::kMap, ST>(r0, rep_ptr(a, 4 * j), a, tp, lane, bm);
+      store_rep<S::kMap, ST>(plane_xor(r0, p1y0), rep_ptr(a, 4 * j + 1), a, tp, lane, bm);
+      const Plane16 r2 = plane_horner_rows<(uint32_t)(4 * j + 2)>(p1y1, p0y1);
+      store_rep<S::kMap, ST>(r2, rep_ptr(a, 4 * j + 2), a, tp, lane, bm);
+      store_rep<S::kMap, ST>(plane_xor(r2, p1y1), rep_ptr(a, 4 * j + 3), a, tp, lane, bm);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    encode_quad_group<K, N, RPW, WV, W, ST, S0 + 1>(set_planes, a, tp, lane, bm);
+  }
+}
+
+template <int K, int N, int RPW, int WV, bool ST, int W>
+__device__ __forceinline__ void quad_dispatch(int wave, const uint32_t *set_planes, const FastEncodeArgs &a, TilePos tp,
+                                              int lane, const BitMasks &bm) {
+  if constexpr (W < WV) {
+    if (wave == W)
+      encode_quad_group<K, N, RPW, WV, W, ST>(set_planes, a, tp, lane, bm);
+    else
+      quad_dispatch<K, N, RPW, WV, ST, W + 1>(wave, set_planes, a, tp, lane, bm);
+  } else {
+    __builtin_unreachable();
+  }
+}
+
+template <int K, int N, int RPW, int WV, bool ST, int W>
+__device__ __forceinline__ void quad_zero_dispatch(int wave, const FastEncodeArgs &a, TilePos tp, int lane,
+                                                   const BitMasks &bm) {
+  using S = EncodeShape<K, N, RPW, WV>;
+  if constexpr (W < WV) {
+    if (wave == W) {
+#pragma unroll
+      for (int s = 0; s < S::kQPW; ++s)
+        if (S::kQuads.j[W][s] >= 0)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            store_rep<S::kMap, ST>(plane_zero(), rep_ptr(a, 4 * S::kQuads.j[W][s] + r), a, tp, lane, bm);
+    } else {
+      quad_zero_dispatch<K, N, RPW, WV, ST, W + 1>(wave, a, tp, lane, bm);
+    }
+  } else {
+    __builtin_unreachable();
+  }
+}
+
 // k = 4: load dwords 2p, 2p+1 of the 32 stripes of set `set`; slot i <->
 // stripe stripe0 + s + 64 i (whole tiles of one object).  The data stays in
 // the loaded vector registers until the next iteration unpacks it, so no copy
@@ -515,8 +687,9 @@ __device__ __forceinline__ void encode_unpack16(const u32x4 (&V)[16], uint32_t (
 
 // STREAM: tiles may straddle objects (groups_per_obj % 16 != 0, k >= 8); the
 // non-stream instantiation keeps one base address per tile.  SPLIT: replica
-// pairs from the one-level split (Taylor coefficients in LDS).
-template <int K, int N, int RPW, int WV, bool STREAM, bool SPLIT>
+// pairs from the one-level split (Taylor coefficients in LDS); QUAD (with
+// SPLIT): replica quads from the two-level split.
+template <int K, int N, int RPW, int WV, bool STREAM, bool SPLIT, bool QUAD = false>
 __global__ __launch_bounds__((EncodeShape<K, N, RPW, WV>::kThreads), (EncodeShape<K, N, RPW, WV>::kWavesPerSimd))
 void k_encode_bs(FastEncodeArgs a) {
   using S = EncodeShape<K, N, RPW, WV>;
@@ -557,7 +730,9 @@ void k_encode_bs(FastEncodeArgs a) {
     // Issuing the same stores here (zeros into this wave's replica cells of
     // its first tile, which that tile overwrites, in order, from the same
     // wave) makes both states alike.
-    if constexpr (SPLIT)
+    if constexpr (QUAD)
+      quad_zero_dispatch<K, N, RPW, WV, STREAM, 0>(wave, a, tile_pos(a, tile), lane, bm);
+    else if constexpr (SPLIT)
       pair_zero_dispatch<K, N, RPW, WV, STREAM, 0>(wave, a, tile_pos(a, tile), lane, bm);
     else
       encode_zero_dispatch<K, N, RPW, WV, STREAM, 0>(wave, a, tile_pos(a, tile), lane, bm);
@@ -598,7 +773,15 @@ void k_encode_bs(FastEncodeArgs a) {
     const uint32_t next = tile + t_step;
     if (next < t_end) load(next);
     // ---- evaluate this wave's replicas and store
-    if constexpr (SPLIT) {
+    if constexpr (QUAD) {
+      taylor_lds<K, N, RPW, WV>(wave, my_set);
+      __syncthreads();
+      quad_twist_lds<K, N, RPW, WV>(wave, my_set);
+      __syncthreads();
+      quad_taylor_lds<K, N, RPW, WV>(wave, my_set);
+      __syncthreads();
+      quad_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
+    } else if constexpr (SPLIT) {
       taylor_lds<K, N, RPW, WV>(wave, my_set);
       __syncthreads();
       pair_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
@@ -609,10 +792,10 @@ void k_encode_bs(FastEncodeArgs a) {
   }
 }
 
-template <int K, int N, int RPW, int WV, bool STREAM, bool SPLIT>
+template <int K, int N, int RPW, int WV, bool STREAM, bool SPLIT, bool QUAD>
 static hipError_t launch_encode_bs_st(const FastEncodeArgs &a, hipStream_t s) {
   using S = EncodeShape<K, N, RPW, WV>;
-  hipError_t e = ensure_lds_attr(&k_encode_bs<K, N, RPW, WV, STREAM, SPLIT>, S::kLdsBytes);
+  hipError_t e = ensure_lds_attr(&k_encode_bs<K, N, RPW, WV, STREAM, SPLIT, QUAD>, S::kLdsBytes);
   if (e != hipSuccess) return e;
   const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
   int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
@@ -620,32 +803,41 @@ static hipError_t launch_encode_bs_st(const FastEncodeArgs &a, hipStream_t s) {
   if (over) grid = (int)over;
   if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_encode_bs<K, N, RPW, WV, STREAM, SPLIT>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
+  hipLaunchKernelGGL((k_encode_bs<K, N, RPW, WV, STREAM, SPLIT, QUAD>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s,
+                     a);
   return hipGetLastError();
 }
 
-// VDS_EC_ENCODE_PATH=horner: plain Horner where split mode is compiled (A/B).
-static bool encode_path_horner() {
-  static const bool h = [] {
+// VDS_EC_ENCODE_PATH=horner: plain Horner where split mode is compiled;
+// =pair: the one-level split where the two-level one is the default (A/B).
+static char encode_path() {
+  static const char h = [] {
     const char *v = std::getenv("VDS_EC_ENCODE_PATH");
-    return v && v[0] == 'h';
+    return v ? v[0] : '\0';
   }();
   return h;
 }
 
-template <int K, int N, int RPW, int WV, bool SPLIT>
+template <int K, int N, int RPW, int WV, bool SPLIT, bool QUAD>
 static hipError_t launch_encode_bs_sp(const FastEncodeArgs &a, hipStream_t s) {
-  if (a.groups_per_obj % 16 == 0) return launch_encode_bs_st<K, N, RPW, WV, false, SPLIT>(a, s);
-  if constexpr (K >= 8) return launch_encode_bs_st<K, N, RPW, WV, true, SPLIT>(a, s);
+  if (a.groups_per_obj % 16 == 0) return launch_encode_bs_st<K, N, RPW, WV, false, SPLIT, QUAD>(a, s);
+  if constexpr (K >= 8) return launch_encode_bs_st<K, N, RPW, WV, true, SPLIT, QUAD>(a, s);
   return hipErrorNotSupported;
 }
 
+// Two-level split for N = 64 (the live shape: +5.5%, same box), one-level for
+// K >= 16 otherwise (two-level measured slower at k = 32 / n = 40, 10.35-10.5
+// vs 10.1-10.15 ms, and at k = 16: DESIGN.md section 3), plain Horner below.
 template <int K, int N, int RPW, int WV>
 static hipError_t launch_encode_bs(const FastEncodeArgs &a, hipStream_t s) {
-  if constexpr (K >= 16) {
-    if (!encode_path_horner()) return launch_encode_bs_sp<K, N, RPW, WV, true>(a, s);
+  if constexpr (K >= 16 && N % 4 == 0) {
+    if (encode_path() == 'q' || (N == 64 && encode_path() == '\0'))
+      return launch_encode_bs_sp<K, N, RPW, WV, true, true>(a, s);
   }
-  return launch_encode_bs_sp<K, N, RPW, WV, false>(a, s);
+  if constexpr (K >= 16) {
+    if (encode_path() != 'h') return launch_encode_bs_sp<K, N, RPW, WV, true, false>(a, s);
+  }
+  return launch_encode_bs_sp<K, N, RPW, WV, false, false>(a, s);
 }
 
 bool has_encode_fast(uint32_t k, uint32_t n) {

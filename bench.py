@@ -397,9 +397,10 @@ def main():
     torch.cuda.synchronize(dev)
     restore_kernel = {4: "jit", 3: "syndrome", 2: "bitsliced", 1: "generic"}[chunk.restore_path(k, nodes, L, padding,
                                                                                              objects)]
-    # correctness guard on the measured buffers (outside the timed region)
-    assert torch.equal(restored[:size], inp[:size]) and torch.equal(restored[-size:], inp[-size:]), \
-        "repair output differs from the input"
+    # correctness guard on the measured buffers (outside the timed region):
+    # every restored object equals its input (a device-side compare of the
+    # whole batch); the parity suite checks the bytes against the oracle
+    assert torch.equal(restored, inp), "repair output differs from the input"
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]

@@ -400,7 +400,10 @@ def main():
     # correctness guard on the measured buffers (outside the timed region):
     # every restored object equals its input (a device-side compare of the
     # whole batch); the parity suite checks the bytes against the oracle
-    assert torch.equal(restored, inp), "repair output differs from the input"
+    # (in 1 GiB slices: torch.equal materialises an element-wise result)
+    sl = 1 << 30
+    assert all(torch.equal(restored[i:i + sl], inp[i:i + sl]) for i in range(0, objects * size, sl)), \
+        "repair output differs from the input"
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]

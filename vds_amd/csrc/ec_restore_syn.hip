@@ -12,6 +12,8 @@
 //   4. big-endian stores through an LDS staging of the tile.
 // REGEN stops after step 2 and writes the recovered points as replica bytes:
 // the fused repair of sync_process.cpp:313-335 (decode + re-encode).
+#include <algorithm>
+
 #include "restore_syn.hpp"
 
 namespace vds_ec {
@@ -87,7 +89,17 @@ hipError_t launch_restore_syn_jit(hipFunction_t fn, uint32_t k, uint32_t n, cons
   if (over) grid = over;
   if (grid > a.total_tiles) grid = a.total_tiles;
   if (grid == 0) return hipSuccess;
-  void *args[] = {const_cast<SynRestoreArgs *>(&a)};
+  // survivors in point order: the scatter fill programs of wave w take the
+  // survivors of rank 4w..4w+3 (vds_ec_jit.cpp)
+  SynRestoreArgs b = a;
+  uint32_t ord[kMaxFastK];
+  for (uint32_t j = 0; j < k; ++j) ord[j] = j;
+  std::sort(ord, ord + k, [&](uint32_t x, uint32_t y) { return a.point[x] < a.point[y]; });
+  for (uint32_t j = 0; j < k; ++j) {
+    b.chunks[j] = a.chunks[ord[j]];
+    b.point[j] = a.point[ord[j]];
+  }
+  void *args[] = {&b};
   return hipModuleLaunchKernel(fn, grid, 1, 1, threads, 1, 1, lds, s, args, nullptr);
 }
 

@@ -365,6 +365,27 @@ __device__ __forceinline__ void lds_xor_point(const SynLds &L, int pt, const Pla
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Scatter fill (FillP::kScatter, vds_ec_jit.cpp): wave W's share of every
+// erased point below K, XORed into the zeroed slots.  Dispatched on a
+// compile-time wave so each arm stores its own results (a runtime switch
+// merged the 64 result registers of all arms and spilled them).
+template <int WV, class FillP, int W>
+__device__ __forceinline__ void syn_scatter_fill(int wave, const SynLds &L) {
+  if constexpr (W < WV) {
+    if (wave != W) return syn_scatter_fill<WV, FillP, W + 1>(wave, L);
+#pragma unroll
+    for (int q = 0; q < FillP::kParts; ++q) {
+      uint32_t acc[16 * FillP::kPart];
+      FillP::fill_part(q, W, L, acc);
+#pragma unroll
+      for (int m = 0; m < FillP::kPart; ++m)
+        if (q * FillP::kPart + m < FillP::kFill)
+          lds_xor_point(L, FillP::kPoint[q * FillP::kPart + m < FillP::kFill ? q * FillP::kPart + m : 0],
+                        *reinterpret_cast<const Plane16 *>(acc + 16 * m));
+    }
+  }
+}
+
 // Batch mode: the last tile of an object may run past its bytes.  Loads
 // beyond `valid` bytes read zeros and stores beyond it write nothing (byte by
 // byte for the one 16-byte piece that straddles the end).
@@ -421,10 +442,12 @@ __device__ __forceinline__ void st16_guard(uint8_t *p, u32x4 v, int64_t valid) {
 // straight from the survivors instead of syndromes + recovery.
 struct NoFill {
   static constexpr int kFill = -1;
+  static constexpr bool kScatter = false;
 };
 template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false, class FillP = NoFill>
 __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   constexpr bool FILL = FillP::kFill >= 0;
+  constexpr bool kScatter = FILL && FillP::kScatter;
   using S = SynShape<K, N, WV>;
   using P = typename S::P;
   constexpr bool kPrio = S::kPrio;
@@ -553,6 +576,13 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) L.put(4 * my_erased + g, z);
       }
+      if constexpr (kScatter) {  // the fill shares meet in these slots (LDS XOR atomics)
+        if (wave < FillP::kFill) {
+          const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int g = 0; g < 4; ++g) L.put(4 * (int)FillP::kPoint[wave < FillP::kFill ? wave : 0] + g, z);
+        }
+      }
       uint64_t bor[2] = {0, 0};  // RT restore: borrowed slots of each half
       if constexpr (RT && !REGEN) {
         bor[0] = s_ld(&half_obj(tile, 0).rt.borrowed);
@@ -680,6 +710,11 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
           }
         }
       }
+    } else if constexpr (kScatter) {
+      // ---- 2''. this wave's survivors' share of every erased point below K
+      // (its own stage-1 slots in, LDS XOR atomics out; survivors sorted by point)
+      syn_scatter_fill<WV, FillP, 0>(wave, L);
+      if (!kLateLoad) prefetch(tile + t_step);
     } else if constexpr (FILL) {
       if (wave < FillP::kFill) {
         uint32_t acc[16];

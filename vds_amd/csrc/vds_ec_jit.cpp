@@ -69,6 +69,15 @@ int fill_block() {
   }();
   return pb;
 }
+// Column-partitioned fill programs (xorprog.hpp emit_fill_scatter; default)
+// or the row form; VDS_EC_JIT_SCATTER=0 selects the row form (A/B).
+bool fill_scatter() {
+  static const bool sc = [] {
+    const char *v = std::getenv("VDS_EC_JIT_SCATTER");
+    return !(v && v[0] == '0');
+  }();
+  return sc;
+}
 bool fill_prefetch() {
   static const bool pf = std::getenv("VDS_EC_JIT_NOPF") == nullptr;
   return pf;
@@ -116,7 +125,10 @@ std::string kernel_source(const Key &key) {
   xorgen::appendf(s, "#define VDS_GM2 %d\n", VDS_GM2);  // (the interpolation this library was built with)
   xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
   xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
-  xorgen::emit_fill_programs(s, "JitFill", K, sp, fill_block(), fill_prefetch());
+  if (fill_scatter())
+    xorgen::emit_fill_scatter(s, "JitFill", K, sp);
+  else
+    xorgen::emit_fill_programs(s, "JitFill", K, sp, fill_block(), fill_prefetch());
   xorgen::appendf(s, "}  // namespace vds_ec\n");
   xorgen::appendf(s,
                   "extern \"C\" __global__ __launch_bounds__((vds_ec::SynShape<%d, %d, %d>::kThreads), "

@@ -18,6 +18,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -343,7 +344,8 @@ inline size_t emit_fill_programs(std::string &s, const char *name, int K, const 
     }
   InputMap im;
   im.map = spoints;
-  appendf(s, "struct %s {\n  static constexpr int kFill = %zu;\n", name, EU.size());
+  appendf(s, "struct %s {\n  static constexpr int kFill = %zu;\n  static constexpr bool kScatter = false;\n", name,
+          EU.size());
   appendf(s, "  static constexpr uint8_t kPoint[%zu] = {", EU.empty() ? (size_t)1 : EU.size());
   for (int e : EU) appendf(s, "%d, ", e);
   appendf(s, "};\n");
@@ -357,6 +359,79 @@ inline size_t emit_fill_programs(std::string &s, const char *name, int K, const 
   appendf(s, "  template <typename In>\n  __device__ __forceinline__ static void fill(int w, const In &IN4, uint32_t (&acc)[16]) {\n");
   appendf(s, "    switch (w) {\n");
   for (size_t m = 0; m < EU.size(); ++m) appendf(s, "      case %zu: fill%zu(IN4, acc); break;\n", m, m);
+  appendf(s, "      default: break;\n    }\n  }\n};\n");
+  return total;
+}
+
+// Column-partitioned fill ("scatter") programs of one survivor set: wave w
+// takes the survivors of rank 4w..4w+3 (spoints ascending; the host sorts
+// the launch's survivors by point, so these are the ones wave w itself
+// stored in stage 1) and computes their share of every erased point below K
+// -- the same Lagrange map as emit_fill_programs, partitioned by columns
+// instead of rows.  The shares meet in LDS through XOR atomics.  Fewer XORs
+// than the row form (k = 16: ~2.1K vs ~2.6K per tile with one Paar block of
+// all four survivors; k = 32: ~6.9K vs ~9.8K, balanced over all waves) and
+// a quarter of its LDS reads.  Programs cover at most kScatterPart erased
+// points each (register pressure).
+constexpr int kScatterPart = 4;
+// survivors per Paar block of a scatter program (VDS_EC_JIT_SPB overrides)
+inline int scatter_block() {
+  const char *v = std::getenv("VDS_EC_JIT_SPB");
+  const int x = v ? std::atoi(v) : 0;
+  return x >= 1 && x <= 4 ? x : 1;
+}
+inline size_t emit_fill_scatter(std::string &s, const char *name, int K, const std::vector<int> &spoints) {
+  std::vector<int> EU;
+  for (int a = 0; a < K; ++a)
+    if (std::find(spoints.begin(), spoints.end(), a) == spoints.end()) EU.push_back(a);
+  const int F = (int)EU.size(), WV = K / 4, parts = (F + kScatterPart - 1) / kScatterPart;
+  std::vector<uint32_t> A((size_t)F * K);
+  for (int m = 0; m < F; ++m)
+    for (int j = 0; j < K; ++j) {
+      uint32_t num = 1, den = 1;
+      for (int t = 0; t < K; ++t)
+        if (t != j) {
+          num = vds_ec::gf16_mul(num, (uint32_t)(EU[m] ^ spoints[t]));
+          den = vds_ec::gf16_mul(den, (uint32_t)(spoints[j] ^ spoints[t]));
+        }
+      A[(size_t)m * K + j] = vds_ec::gf16_mul(num, vds_ec::gf16_inv(den));
+    }
+  const auto rows = all_bitrows(A, F, K);
+  appendf(s, "struct %s {\n  static constexpr int kFill = %d;\n  static constexpr bool kScatter = true;\n", name, F);
+  appendf(s, "  static constexpr int kParts = %d, kPart = %d;\n", parts, kScatterPart);
+  appendf(s, "  static constexpr uint8_t kPoint[%d] = {", F ? F : 1);
+  for (int e : EU) appendf(s, "%d, ", e);
+  appendf(s, "};\n");
+  size_t total = 0;
+  for (int w = 0; w < WV; ++w)
+    for (int q = 0; q < parts; ++q) {
+      const int m0 = q * kScatterPart, m1 = std::min(F, m0 + kScatterPart);
+      std::vector<std::vector<int>> sub;
+      for (int r = 16 * m0; r < 16 * m1; ++r) {
+        std::vector<int> row;
+        for (int x : rows[r])
+          if (x >= 64 * w && x < 64 * w + 64) row.push_back(x - 64 * w);
+        sub.push_back(row);
+      }
+      char nm[48];
+      std::snprintf(nm, sizeof nm, "fill%d_%d", w, q);
+      InputMap im;  // (this wave's survivors, in their own LDS slots)
+      for (int i = 0; i < 4; ++i) im.map.push_back(spoints[4 * w + i]);
+      total += emit_program(s, nm, sub, 4, row_range(0, (int)sub.size()), scatter_block(), im);
+    }
+  for (int q = 0; q < parts; ++q) {
+    appendf(s, "  template <typename In>\n  __device__ __forceinline__ static void fill_part%d(int w, const In &IN4, uint32_t (&acc)[%d]) {\n",
+            q, 16 * kScatterPart);
+    appendf(s, "    switch (w) {\n");
+    for (int w = 0; w < WV; ++w)
+      appendf(s, "      case %d: fill%d_%d(IN4, reinterpret_cast<uint32_t(&)[%d]>(acc)); break;\n", w, w, q,
+              16 * (std::min(F, q * kScatterPart + kScatterPart) - q * kScatterPart));
+    appendf(s, "      default: break;\n    }\n  }\n");
+  }
+  appendf(s, "  template <typename In>\n  __device__ __forceinline__ static void fill_part(int q, int w, const In &IN4, uint32_t (&acc)[%d]) {\n",
+          16 * kScatterPart);
+  appendf(s, "    switch (q) {\n");
+  for (int q = 0; q < parts; ++q) appendf(s, "      case %d: fill_part%d(w, IN4, acc); break;\n", q, q);
   appendf(s, "      default: break;\n    }\n  }\n};\n");
   return total;
 }

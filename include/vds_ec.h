@@ -288,8 +288,9 @@ int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void
  * VDS_EC_RESTORE_PATH=bs in the environment disables path 3 (A/B).          */
 int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint64_t size);
 int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size, uint16_t padding, uint32_t count);
-/* 3 = the regenerate rides the syndrome kernel (every target an erased point
- * of a compiled (k, n)) for the full tiles, 2 = the runtime-coefficient
+/* 4 = the regenerate runs the survivor set's run-time compiled kernel
+ * (vds_ec_jit_*), 3 = the regenerate rides the syndrome kernel (every target
+ * an erased point of a compiled (k, n)) for the full tiles, 2 = the runtime-coefficient
  * bit-sliced kernel (k in {16, 32}, at most k targets, >= 512 full stripes),
  * 1 = generic path only.                                                    */
 int vds_ec_regenerate16_path(uint16_t k, const uint16_t *nodes, const uint16_t *targets, uint32_t ntargets,

@@ -150,3 +150,59 @@ def test_jit_background_mode_switches_after_second_use(gpu):
         assert _path(k, nodes, L) == 4
     finally:
         chunk.jit_set_mode(0)
+
+
+def _path_regen(k, nodes, targets, L):
+    from vds_amd import _lib
+    nd = np.array(nodes, dtype=np.uint16)
+    tg = np.array(targets, dtype=np.uint16)
+    return _lib.lib().vds_ec_regenerate16_path(k, nd.ctypes.data_as(_lib.u16p), tg.ctypes.data_as(_lib.u16p),
+                                               len(targets), L)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,erased,targets,T", [
+    (16, (0, 5, 10, 15), [15, 0], 2 * 2048 + 3),
+    (16, (1, 2, 17, 19), [2, 17, 19], 2048),          # targets beyond k (no interpolation point)
+    (32, (0, 5, 10, 15, 20, 25, 30, 35), [35, 0, 20], 2048 * 2 + 1),
+])
+@pytest.mark.parametrize("codeword", [True, False])
+def test_jit_regenerate_vs_oracle(jit_sync, k, erased, targets, T, codeword):
+    """The regenerate kernel compiled for the survivor set (targets: every
+    erased point) against the oracle's restore -> re-encode route, codewords
+    and random survivors (trailer only on the first), two objects at a stride."""
+    import torch
+    from vds_amd import chunk
+    n = k + k // 4
+    nodes = _nodes(n, erased)
+    rng = np.random.default_rng(T + k + codeword)
+    L = 2 * T + 2
+    p = (2 * k - 3) if not codeword else 0
+    objs = []
+    for o in range(2):
+        if codeword:
+            d = O.splitmix(SEED + 3300 + o, 2 * k * T)
+            objs.append([O.encode(k, r, d) for r in nodes])
+        else:
+            sv = [rng.integers(0, 256, L, dtype=np.uint8) for _ in nodes]
+            sv[0][-2], sv[0][-1] = p >> 8, p & 0xFF
+            objs.append(sv)
+    stride = L + 4
+    host = np.zeros((k, 2, stride), dtype=np.uint8)
+    for o, sv in enumerate(objs):
+        for j, b in enumerate(sv):
+            host[j, o, :L] = b
+    dev = torch.from_numpy(host).cuda()
+    ostride = L + 8
+    outs = torch.full((len(targets), 2, ostride), 0x5A, dtype=torch.uint8, device="cuda")
+    chunk.regenerate_device(k, nodes, [dev[j].data_ptr() for j in range(k)], L, stride, 2, targets,
+                            [outs[i].data_ptr() for i in range(len(targets))], ostride)
+    torch.cuda.synchronize()
+    assert _path_regen(k, nodes, targets, L) == 4
+    got = outs.cpu().numpy()
+    for o in range(2):
+        rest = O.restore(k, nodes, objs[o])
+        for i, t in enumerate(targets):
+            want = O.encode(k, t, rest)
+            assert np.array_equal(got[i, o, :L], want), (o, t)
+            assert (got[i, o, L:] == 0x5A).all()

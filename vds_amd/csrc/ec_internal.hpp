@@ -247,7 +247,9 @@ hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, h
 // The run-time compiled restore kernel of a's survivor set (vds_ec_jit.cpp) on
 // the current device, or nullptr (disabled, not compiled yet -- then queued --
 // or failed): a.point[0..k) set by the plan.
-hipFunction_t jit_restore_function(uint32_t k, uint32_t n, const SynRestoreArgs &a);
+hipFunction_t jit_restore_function(uint32_t k, uint32_t n, const SynRestoreArgs &a, bool regen = false);
+// the set's kernel is loaded and the module is enabled (path queries)
+bool jit_ready(uint32_t k, uint32_t n, const SynRestoreArgs &a, bool regen);
 bool jit_enabled();  // mode != 0 (vds_ec_jit_set_mode)
 hipError_t launch_restore_syn_jit(hipFunction_t fn, uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s);
 // a.objs / a.plans / a.tiles / a.total_tiles set; the other fields unused

@@ -963,7 +963,8 @@ int regenerate_device(unsigned cb, uint32_t k, const uint16_t *nodes, const uint
       sa.regen_stride = out_stride;
       sa.tiles_per_obj = (uint32_t)tiles;
       sa.total_tiles = (uint32_t)total;
-      hipError_t e = launch_restore_syn(k, syn_n, sa, s, true);
+      const hipFunction_t jf = jit_restore_function(k, syn_n, sa, true);  // (the set's own kernel, vds_ec_jit.cpp)
+      hipError_t e = jf ? launch_restore_syn_jit(jf, k, syn_n, sa, s) : launch_restore_syn(k, syn_n, sa, s, true);
       if (e != hipSuccess) return hip_status(e);
       fast_stripes = tiles * kTileStripes;
       parts[0].t_begin = fast_stripes;
@@ -2619,7 +2620,7 @@ int vds_ec_regenerate16_path(uint16_t k, const uint16_t *nodes, const uint16_t *
       }
     syn = hit;
   }
-  if (syn) return 3;
+  if (syn) return jit_ready(k, n, sa, true) ? 4 : 3;
   const uint64_t gpo = T % 512 == 0 ? T / 512 : 4 * (T / kTileStripes);
   return (has_restore_fast(k) && ntargets <= k && gpo > 0) ? 2 : 1;
 }

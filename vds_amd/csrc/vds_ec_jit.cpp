@@ -103,7 +103,10 @@ constexpr size_t kJitMaxSeen = 1 << 14;  // sighting counts kept (cleared when f
 struct Key {
   uint32_t k, n;
   uint64_t survivors;  // bit a: point a survives
-  bool operator<(const Key &o) const { return std::tie(k, n, survivors) < std::tie(o.k, o.n, o.survivors); }
+  uint32_t regen = 0;  // 1: the regenerate kernel (targets: every erased point)
+  bool operator<(const Key &o) const {
+    return std::tie(k, n, survivors, regen) < std::tie(o.k, o.n, o.survivors, o.regen);
+  }
 };
 
 struct Entry {
@@ -125,17 +128,23 @@ std::string kernel_source(const Key &key) {
   xorgen::appendf(s, "#define VDS_GM2 %d\n", VDS_GM2);  // (the interpolation this library was built with)
   xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
   xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
-  if (fill_scatter())
+  if (key.regen) {  // every erased point, in ascending order (= SynRestoreArgs::erased)
+    std::vector<int> tg;
+    for (int a = 0; a < N; ++a)
+      if (!((key.survivors >> a) & 1u)) tg.push_back(a);
+    xorgen::emit_fill_scatter(s, "JitFill", K, sp, &tg);
+  } else if (fill_scatter()) {
     xorgen::emit_fill_scatter(s, "JitFill", K, sp);
-  else
+  } else {
     xorgen::emit_fill_programs(s, "JitFill", K, sp, fill_block(), fill_prefetch());
+  }
   xorgen::appendf(s, "}  // namespace vds_ec\n");
   xorgen::appendf(s,
                   "extern \"C\" __global__ __launch_bounds__((vds_ec::SynShape<%d, %d, %d>::kThreads), "
                   "(vds_ec::SynShape<%d, %d, %d>::kWavesPerSimd))\n"
                   "void vds_ec_jit_restore(vds_ec::SynRestoreArgs a) {\n"
-                  "  vds_ec::restore_syn_body<%d, %d, %d, false, false, false, vds_ec::JitFill>(a);\n}\n",
-                  K, N, WV, K, N, WV, K, N, WV);
+                  "  vds_ec::restore_syn_body<%d, %d, %d, %s, false, false, vds_ec::JitFill>(a);\n}\n",
+                  K, N, WV, K, N, WV, K, N, WV, key.regen ? "true" : "false");
   return s;
 }
 
@@ -207,7 +216,8 @@ bool compile(const Key &key, std::vector<char> &code, std::string &log) {
   // VDS_EC_JIT_DUMP=<dir>: keep the source and code object (inspection)
   if (const char *dump = std::getenv("VDS_EC_JIT_DUMP")) {
     char base[512];
-    std::snprintf(base, sizeof base, "%s/jit_%u_%u_%llx", dump, key.k, key.n, (unsigned long long)key.survivors);
+    std::snprintf(base, sizeof base, "%s/jit_%u_%u_%llx%s", dump, key.k, key.n, (unsigned long long)key.survivors,
+                  key.regen ? "_regen" : "");
     if (FILE *f = std::fopen((std::string(base) + ".hip").c_str(), "w")) {
       std::fwrite(src.data(), 1, src.size(), f);
       std::fclose(f);
@@ -357,8 +367,8 @@ class Jit {
   bool stop_ = false;
 };
 
-Key key_of(uint32_t k, uint32_t n, const uint8_t *points) {
-  Key key{k, n, 0};
+Key key_of(uint32_t k, uint32_t n, const uint8_t *points, bool regen) {
+  Key key{k, n, 0, regen ? 1u : 0u};
   for (uint32_t j = 0; j < k; ++j) key.survivors |= 1ull << points[j];
   return key;
 }
@@ -367,9 +377,13 @@ Key key_of(uint32_t k, uint32_t n, const uint8_t *points) {
 
 bool jit_enabled() { return jit_mode() != 0; }
 
-hipFunction_t jit_restore_function(uint32_t k, uint32_t n, const SynRestoreArgs &a) {
+hipFunction_t jit_restore_function(uint32_t k, uint32_t n, const SynRestoreArgs &a, bool regen) {
   if (jit_mode() == 0 || !has_restore_syn(k, n)) return nullptr;
-  return Jit::get().function(key_of(k, n, a.point));
+  return Jit::get().function(key_of(k, n, a.point, regen));
+}
+
+bool jit_ready(uint32_t k, uint32_t n, const SynRestoreArgs &a, bool regen) {
+  return jit_mode() != 0 && has_restore_syn(k, n) && Jit::get().ready(key_of(k, n, a.point, regen));
 }
 
 }  // namespace vds_ec

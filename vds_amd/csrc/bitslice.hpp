@@ -181,6 +181,13 @@ VDS_INLINE uint32_t fold_row(uint32_t v, const Plane16 &acc) {
 // which has no standard library headers)
 template <class T, T... I>
 struct IntSeq {};
+#if defined(__clang__)
+template <int N>
+using IntSeqN = __make_integer_seq<IntSeq, int, N>;
+#else  // (g++: the host build of tests/cpp/test_bitslice.cpp)
+template <int N>
+using IntSeqN = IntSeq<int, __integer_pack(N)...>;
+#endif
 
 template <uint32_t C, int... I>
 VDS_INLINE Plane16 row_horner_impl(const Plane16 &acc, const Plane16 &x, IntSeq<int, I...>) {
@@ -200,7 +207,7 @@ VDS_INLINE Plane16 plane_horner_rows(const Plane16 &acc, const Plane16 &x) {
   if constexpr (C == 0)
     return x;
   else
-    return row_horner_impl<C>(acc, x, __make_integer_seq<IntSeq, int, 16>{});
+    return row_horner_impl<C>(acc, x, IntSeqN<16>{});
 }
 
 // Multiply by a wave-uniform runtime constant c (< 2^16): Horner over all 16

@@ -356,13 +356,36 @@ __device__ __forceinline__ void rec_dual(Plane16 &acc, const Plane16 &t, const P
 
 // LDS XOR of a point's sixteen planes (this lane's 64 bytes) as eight
 // ds_xor_b64: planes 4g..4g+3 of point pt at byte (4 pt + g) 1 KiB + 16 lane.
+// With every lane on the same 8-byte half of its 16-byte slot, lanes 8 or 16
+// apart hit the same banks (2-way: +512 conflict cycles per tile in the
+// survivor-set kernel, round 3).  VDS_LDS_XOR_SWZ: a lane whose bits 3 and 4
+// differ takes the other half first, so the lanes of a 16-lane group (banks
+// (a/4) mod 32, as ds_write_b64) and of a 32-lane group (mod 64, as
+// ds_read_b64) cover distinct banks; the data follows with v_cndmask.
+#ifndef VDS_LDS_XOR_SWZ
+#define VDS_LDS_XOR_SWZ 1
+#endif
+#ifndef VDS_COPYOUT_VOLATILE  // (k = 16 copy-out reads: see the staging below; empty = ds_read2_b64, A/B)
+#define VDS_COPYOUT_VOLATILE volatile
+#endif
 __device__ __forceinline__ void lds_xor_point(const SynLds &L, int pt, const Plane16 &v) {
   __attribute__((address_space(3))) uint64_t *dst =
       (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * pt);
+  if constexpr (VDS_LDS_XOR_SWZ != 0) {
+    const uint32_t sw = ((L.lo >> 7) ^ (L.lo >> 8)) & 1u;  // bit 3 ^ bit 4 of the lane (L.lo = 16 lane)
 #pragma unroll
-  for (int h = 0; h < 8; ++h)
-    __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1), (uint64_t)v.p[2 * h] | ((uint64_t)v.p[2 * h + 1] << 32),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (int g = 0; g < 4; ++g) {
+      const uint64_t a = (uint64_t)v.p[4 * g] | ((uint64_t)v.p[4 * g + 1] << 32);
+      const uint64_t b = (uint64_t)v.p[4 * g + 2] | ((uint64_t)v.p[4 * g + 3] << 32);
+      __hip_atomic_fetch_xor(dst + 128 * g + sw, sw ? b : a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_xor(dst + 128 * g + (sw ^ 1u), sw ? a : b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < 8; ++h)
+      __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1), (uint64_t)v.p[2 * h] | ((uint64_t)v.p[2 * h + 1] << 32),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
 }
 
 // Scatter fill (FillP::kScatter, vds_ec_jit.cpp): wave W's share of every
@@ -910,10 +933,14 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
         // half c%2, at 16 c + 8 (c / 16) = r0 + 1056 i
         const lds_char *r0 = L.base + 1056u * kChunks * wave + 16u * lane + 8u * (lane >> 4);
         const auto [g0, out_valid, guard] = target();
+        // (two volatile ds_read_b64, not one ds_read2_b64: 2 + 2 LDS cycles,
+        // banks (a/4) mod 64 over 32 lanes, where the padding after 16 chunks
+        // already puts lanes l and l + 16 on different banks; ds_read2_b64 is
+        // 8 cycles, (a/4) mod 32 over 16 lanes, and 2-way at lanes l, l + 8)
         auto piece = [&](int i) {
           const lds_char *r = r0 + 1056 * i;
-          const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
-          const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
+          const u32x2 v0 = *(__attribute__((address_space(3))) const VDS_COPYOUT_VOLATILE u32x2 *)r;
+          const u32x2 v1 = *(__attribute__((address_space(3))) const VDS_COPYOUT_VOLATILE u32x2 *)(r + 8);
           return u32x4{v0[0], v0[1], v1[0], v1[1]};
         };
         if (!guard) {

@@ -46,8 +46,16 @@
 extern char **environ;
 
 #ifndef VDS_GM2
-#define VDS_GM2 1  // (restore_syn.hpp's default)
+#define VDS_GM2 1  // (restore_syn.hpp's defaults)
 #endif
+#ifndef VDS_LDS_XOR_SWZ
+#define VDS_LDS_XOR_SWZ 1
+#endif
+#ifndef VDS_COPYOUT_VOLATILE
+#define VDS_COPYOUT_VOLATILE volatile
+#endif
+#define VDS_STR2(x) #x
+#define VDS_STR(x) VDS_STR2(x)
 
 namespace vds_ec {
 namespace {
@@ -125,7 +133,8 @@ std::string kernel_source(const Key &key) {
   for (int a = 0; a < N; ++a)
     if ((key.survivors >> a) & 1u) sp.push_back(a);
   std::string s;
-  xorgen::appendf(s, "#define VDS_GM2 %d\n", VDS_GM2);  // (the interpolation this library was built with)
+  xorgen::appendf(s, "#define VDS_GM2 %d\n#define VDS_LDS_XOR_SWZ %d\n#define VDS_COPYOUT_VOLATILE %s\n", VDS_GM2,
+                  VDS_LDS_XOR_SWZ, VDS_STR(VDS_COPYOUT_VOLATILE));  // (the forms this library was built with)
   xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
   xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
   if (key.regen) {  // every erased point, in ascending order (= SynRestoreArgs::erased)

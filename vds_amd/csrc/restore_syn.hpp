@@ -358,15 +358,17 @@ __device__ __forceinline__ void rec_dual(Plane16 &acc, const Plane16 &t, const P
 // ds_xor_b64: planes 4g..4g+3 of point pt at byte (4 pt + g) 1 KiB + 16 lane.
 // With every lane on the same 8-byte half of its 16-byte slot, lanes 8 or 16
 // apart hit the same banks (2-way: +512 conflict cycles per tile in the
-// survivor-set kernel, round 3).  VDS_LDS_XOR_SWZ: a lane whose bits 3 and 4
-// differ takes the other half first, so the lanes of a 16-lane group (banks
-// (a/4) mod 32, as ds_write_b64) and of a 32-lane group (mod 64, as
-// ds_read_b64) cover distinct banks; the data follows with v_cndmask.
+// survivor-set kernel, round 3).  VDS_LDS_XOR_SWZ=1: a lane whose bits 3 and
+// 4 differ takes the other half first (distinct banks per 16- and 32-lane
+// group; the data follows with v_cndmask).  It removed every conflict
+// (SQ_LDS_BANK_CONFLICT 0) and was slower: same box, k = 16 repair 13.99-
+// 14.04 -> 14.17-14.33 ms with the split copy-out reads below, k = 32 9.67 ->
+// 10.41 ms (profiles/round3/ab/swz_ab.log).  Off by default.
 #ifndef VDS_LDS_XOR_SWZ
-#define VDS_LDS_XOR_SWZ 1
+#define VDS_LDS_XOR_SWZ 0
 #endif
-#ifndef VDS_COPYOUT_VOLATILE  // (k = 16 copy-out reads: see the staging below; empty = ds_read2_b64, A/B)
-#define VDS_COPYOUT_VOLATILE volatile
+#ifndef VDS_COPYOUT_VOLATILE  // (k = 16 copy-out reads: see the staging below; volatile = two ds_read_b64, A/B)
+#define VDS_COPYOUT_VOLATILE
 #endif
 __device__ __forceinline__ void lds_xor_point(const SynLds &L, int pt, const Plane16 &v) {
   __attribute__((address_space(3))) uint64_t *dst =
@@ -933,10 +935,10 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
         // half c%2, at 16 c + 8 (c / 16) = r0 + 1056 i
         const lds_char *r0 = L.base + 1056u * kChunks * wave + 16u * lane + 8u * (lane >> 4);
         const auto [g0, out_valid, guard] = target();
-        // (two volatile ds_read_b64, not one ds_read2_b64: 2 + 2 LDS cycles,
-        // banks (a/4) mod 64 over 32 lanes, where the padding after 16 chunks
-        // already puts lanes l and l + 16 on different banks; ds_read2_b64 is
-        // 8 cycles, (a/4) mod 32 over 16 lanes, and 2-way at lanes l, l + 8)
+        // (the compiler merges the two halves into one ds_read2_b64: 8 LDS
+        // cycles, banks (a/4) mod 32 over 16 lanes, 2-way at lanes l, l + 8;
+        // as two volatile ds_read_b64 -- 2 + 2 cycles, conflict-free thanks to
+        // the padding -- they measured slower, VDS_COPYOUT_VOLATILE)
         auto piece = [&](int i) {
           const lds_char *r = r0 + 1056 * i;
           const u32x2 v0 = *(__attribute__((address_space(3))) const VDS_COPYOUT_VOLATILE u32x2 *)r;

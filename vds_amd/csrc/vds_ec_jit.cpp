@@ -49,10 +49,10 @@ extern char **environ;
 #define VDS_GM2 1  // (restore_syn.hpp's defaults)
 #endif
 #ifndef VDS_LDS_XOR_SWZ
-#define VDS_LDS_XOR_SWZ 1
+#define VDS_LDS_XOR_SWZ 0
 #endif
 #ifndef VDS_COPYOUT_VOLATILE
-#define VDS_COPYOUT_VOLATILE volatile
+#define VDS_COPYOUT_VOLATILE
 #endif
 #define VDS_STR2(x) #x
 #define VDS_STR(x) VDS_STR2(x)

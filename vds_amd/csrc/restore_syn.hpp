@@ -239,6 +239,15 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
 #ifndef VDS_GM2
 #define VDS_GM2 1
 #endif
+// Phases of the two-level interpolation run at wave priority 1 (bit 0: S1,
+// bit 1: S2, bit 2: S3; two workgroups per CU only, see syn_prio).
+#ifndef VDS_GM2_PRIO
+#define VDS_GM2_PRIO 1
+#endif
+// The survivor-set kernel's scatter fill at wave priority 1 (A/B).
+#ifndef VDS_FILL_PRIO
+#define VDS_FILL_PRIO 0
+#endif
 template <int K, int N, int WV, int W>
 __device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
   using P = RestorePrograms<K, N, WV>;
@@ -249,35 +258,41 @@ __device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, uint32
     uint32_t acc[64];
     auto cell = [&](int c) -> uint32_t(&)[16] { return *reinterpret_cast<uint32_t(*)[16]>(acc + 16 * c); };
     // S1: levels 1 and 2 on this wave's slots 4W..4W+3 (only this wave touches them)
-    syn_prio<1, kPrio>();
+    syn_prio<1, kPrio && (VDS_GM2_PRIO & 1)>();
     P::gm_s1_(W, L, acc);
 #pragma unroll
     for (int c = 0; c < 4; ++c) syn_put_point(L, 4 * W + c, cell(c));
-    syn_prio<0, kPrio>();
+    syn_prio<0, kPrio && (VDS_GM2_PRIO & 1)>();
     st.mark(7);
     __syncthreads();
     st.mark(8);
     // S2: family f = W / kWpf (slots 4j + f), coefficients c0.. -> slot 4c + f
+    syn_prio<1, kPrio && (VDS_GM2_PRIO & 2)>();
     P::gm_s2_(W, L, acc);
     constexpr int f = W / kWpf, c0 = 4 * (W % kWpf);
     if constexpr (kWpf > 1) __syncthreads();  // (every wave of the family has read it)
 #pragma unroll
     for (int c = 0; c < 4; ++c) syn_put_point(L, 4 * (c0 + c) + f, cell(c));
+    syn_prio<0, kPrio && (VDS_GM2_PRIO & 2)>();
     st.mark(9);
     __syncthreads();
     st.mark(10);
     // S3: Q_par coefficients i0.. (expansion sums, then the twists) -> slot H par + i
+    syn_prio<1, kPrio && (VDS_GM2_PRIO & 4)>();
     P::gm_s3sum_(W, L, acc);
     constexpr int par = W / kWpq, i0 = 4 * (W % kWpq);
 #pragma unroll
     for (int c = 0; c < 4; ++c) P::gm_twist(i0 + c, cell(c));
+    syn_prio<0, kPrio && (VDS_GM2_PRIO & 4)>();
     __syncthreads();  // every wave has read the R coefficients
 #pragma unroll
     for (int c = 0; c < 4; ++c) syn_put_point(L, H * par + i0 + c, cell(c));
     st.mark(11);
     __syncthreads();
     st.mark(12);
+    syn_prio<1, kPrio && (VDS_GM2_PRIO & 8)>();
     syn_gm_stage_c<K, W, K / WV>(L, cells);
+    syn_prio<0, kPrio && (VDS_GM2_PRIO & 8)>();
     st.mark(13);
   }
 }
@@ -738,7 +753,9 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     } else if constexpr (kScatter) {
       // ---- 2''. this wave's survivors' share of every erased point below K
       // (its own stage-1 slots in, LDS XOR atomics out; survivors sorted by point)
+      syn_prio<1, kPrio && (VDS_FILL_PRIO != 0)>();
       syn_scatter_fill<WV, FillP, 0>(wave, L);
+      syn_prio<0, kPrio && (VDS_FILL_PRIO != 0)>();
       if (!kLateLoad) prefetch(tile + t_step);
     } else if constexpr (FILL) {
       if (wave < FillP::kFill) {

@@ -51,6 +51,12 @@ extern char **environ;
 #ifndef VDS_LDS_XOR_SWZ
 #define VDS_LDS_XOR_SWZ 0
 #endif
+#ifndef VDS_GM2_PRIO
+#define VDS_GM2_PRIO 1
+#endif
+#ifndef VDS_FILL_PRIO
+#define VDS_FILL_PRIO 0
+#endif
 #ifndef VDS_COPYOUT_VOLATILE
 #define VDS_COPYOUT_VOLATILE
 #endif
@@ -133,8 +139,11 @@ std::string kernel_source(const Key &key) {
   for (int a = 0; a < N; ++a)
     if ((key.survivors >> a) & 1u) sp.push_back(a);
   std::string s;
-  xorgen::appendf(s, "#define VDS_GM2 %d\n#define VDS_LDS_XOR_SWZ %d\n#define VDS_COPYOUT_VOLATILE %s\n", VDS_GM2,
-                  VDS_LDS_XOR_SWZ, VDS_STR(VDS_COPYOUT_VOLATILE));  // (the forms this library was built with)
+  xorgen::appendf(s,
+                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n#define VDS_FILL_PRIO %d\n#define VDS_LDS_XOR_SWZ %d\n"
+                  "#define VDS_COPYOUT_VOLATILE %s\n",
+                  VDS_GM2, VDS_GM2_PRIO, VDS_FILL_PRIO, VDS_LDS_XOR_SWZ,
+                  VDS_STR(VDS_COPYOUT_VOLATILE));  // (the forms this library was built with)
   xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
   xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
   if (key.regen) {  // every erased point, in ascending order (= SynRestoreArgs::erased)

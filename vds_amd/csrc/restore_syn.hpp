@@ -240,9 +240,12 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
 #define VDS_GM2 1
 #endif
 // Phases of the two-level interpolation run at wave priority 1 (bit 0: S1,
-// bit 1: S2, bit 2: S3; two workgroups per CU only, see syn_prio).
+// bit 1: S2, bit 2: S3, bit 3: stage C; two workgroups per CU only, see
+// syn_prio).  Same box, k = 16 repair at 512 x 64 MiB: S1 alone 14.19-14.30
+// ms, S1 + stage C 14.05-14.10 (default); none 15.0-15.15; S2 or S3 added
+// 14.67-14.88 (profiles/round3/ab/gm2_prio_ab.log, prio2_ab.log).
 #ifndef VDS_GM2_PRIO
-#define VDS_GM2_PRIO 1
+#define VDS_GM2_PRIO 9
 #endif
 // The survivor-set kernel's scatter fill at wave priority 1 (A/B).
 #ifndef VDS_FILL_PRIO

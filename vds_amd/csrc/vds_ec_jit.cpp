@@ -52,7 +52,7 @@ extern char **environ;
 #define VDS_LDS_XOR_SWZ 0
 #endif
 #ifndef VDS_GM2_PRIO
-#define VDS_GM2_PRIO 1
+#define VDS_GM2_PRIO 9
 #endif
 #ifndef VDS_FILL_PRIO
 #define VDS_FILL_PRIO 0

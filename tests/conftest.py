@@ -15,6 +15,10 @@ for p in (ROOT, TESTS):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# the tests exercise the run-time compiler itself, not the on-disk cache of
+# its outputs (tests/test_jit_gpu.py covers the cache in its own processes)
+os.environ["VDS_EC_JIT_CACHE"] = "0"
+
 
 def _dump_runtime_libs():
     """At exit, record which ROCm shared objects are mapped (one HIP runtime expected)."""

@@ -40,6 +40,24 @@ def test_jit_build_rejects_sets_outside_the_syndrome_points(vds_lib):
             chunk.jit_build(k, nodes)
 
 
+def test_jit_disk_cache_across_processes(vds_lib, tmp_path):
+    """VDS_EC_JIT_CACHE: the first process compiles and stores the code
+    object; a second process loads the same bytes without the compiler."""
+    import os
+    import subprocess
+    import sys
+    script = ("from vds_amd import chunk, _lib; _lib.lib();"
+              "print(chunk.jit_build(16, [r for r in range(20) if r not in (2, 7, 12, 17)]))")
+    env = dict(os.environ, VDS_EC_JIT_CACHE=str(tmp_path))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sizes = [int(subprocess.run([sys.executable, "-c", script], env=env, cwd=root, check=True,
+                                capture_output=True, text=True, timeout=300).stdout.split()[-1])
+             for _ in range(2)]
+    files = list(tmp_path.glob("*.co"))
+    assert len(files) == 1 and sizes[0] == sizes[1] == files[0].stat().st_size > 10000
+    assert not list(tmp_path.glob("*.tmp"))
+
+
 @pytest.fixture
 def jit_sync(gpu):
     from vds_amd import chunk

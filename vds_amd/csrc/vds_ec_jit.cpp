@@ -21,6 +21,7 @@
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <spawn.h>
+#include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -187,6 +188,54 @@ std::string read_file(const std::string &path) {
   return out;
 }
 
+// On-disk cache of compiled kernels, shared by processes (e.g. the ranks of
+// one node): $VDS_EC_JIT_CACHE, else $XDG_CACHE_HOME/vds_ec, else
+// $HOME/.cache/vds_ec; VDS_EC_JIT_CACHE=0 disables it.  A file is named by a
+// hash of the kernel source (which carries the programs and every build
+// switch) and of the helper's size and mtime (which carries the embedded
+// device headers); it is written to a temporary name and renamed, so readers
+// never see a partial file.
+std::string cache_dir() {
+  static const std::string d = [] {
+    const char *v = std::getenv("VDS_EC_JIT_CACHE");
+    if (v && !std::strcmp(v, "0")) return std::string();
+    std::string dir;
+    if (v && *v) {
+      dir = v;
+    } else if (const char *x = std::getenv("XDG_CACHE_HOME"); x && *x) {
+      dir = std::string(x) + "/vds_ec";
+    } else if (const char *h = std::getenv("HOME"); h && *h) {
+      dir = std::string(h) + "/.cache";
+      (void)mkdir(dir.c_str(), 0700);
+      dir += "/vds_ec";
+    } else {
+      return std::string();
+    }
+    (void)mkdir(dir.c_str(), 0700);
+    return access(dir.c_str(), W_OK) == 0 ? dir : std::string();
+  }();
+  return d;
+}
+
+uint64_t fnv1a(const void *p, size_t n, uint64_t h = 1469598103934665603ull) {
+  const unsigned char *b = static_cast<const unsigned char *>(p);
+  for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+
+std::string cache_path(const std::string &src, const std::string &helper) {
+  const std::string dir = cache_dir();
+  if (dir.empty()) return {};
+  struct stat st {};
+  if (stat(helper.c_str(), &st) != 0) return {};
+  uint64_t h = fnv1a(src.data(), src.size());
+  const int64_t id[2] = {(int64_t)st.st_size, (int64_t)st.st_mtime};
+  h = fnv1a(id, sizeof id, h);
+  char name[64];
+  std::snprintf(name, sizeof name, "/%016llx.co", (unsigned long long)h);
+  return dir + name;
+}
+
 // Compile one survivor set's kernel with the helper (host only: no device
 // needed): source and code object pass through a private temporary directory.
 bool compile(const Key &key, std::vector<char> &code, std::string &log) {
@@ -195,6 +244,14 @@ bool compile(const Key &key, std::vector<char> &code, std::string &log) {
   if (helper.empty() || access(helper.c_str(), X_OK) != 0) {
     log = "vds_ec_jitc not found next to libvds_ec.so";
     return false;
+  }
+  const std::string cached = cache_path(src, helper);
+  if (!cached.empty()) {
+    const std::string bytes = read_file(cached);
+    if (!bytes.empty()) {
+      code.assign(bytes.begin(), bytes.end());
+      return true;
+    }
   }
   const char *tmpenv = std::getenv("TMPDIR");
   std::string dir = std::string(tmpenv && *tmpenv ? tmpenv : "/tmp") + "/vds_ec_jit_XXXXXX";
@@ -250,6 +307,16 @@ bool compile(const Key &key, std::vector<char> &code, std::string &log) {
   std::remove(out.c_str());
   std::remove(err.c_str());
   rmdir(dir.c_str());
+  if (ok && !cached.empty()) {  // (best effort)
+    const std::string tmp = cached + "." + std::to_string((long)getpid()) + ".tmp";
+    if (FILE *f = std::fopen(tmp.c_str(), "wb")) {
+      const bool w = std::fwrite(code.data(), 1, code.size(), f) == code.size();
+      if (std::fclose(f) == 0 && w)
+        (void)std::rename(tmp.c_str(), cached.c_str());
+      else
+        std::remove(tmp.c_str());
+    }
+  }
   return ok;
 }
 

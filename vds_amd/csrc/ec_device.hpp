@@ -20,6 +20,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const volatile u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) volatile u32x4 lds_v4;
+typedef __attribute__((address_space(3))) volatile u32x2 lds_v2;
 typedef __attribute__((address_space(3))) char lds_char;
 
 // Streaming (non-temporal) global accesses of the data path, by bit:

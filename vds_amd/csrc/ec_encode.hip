@@ -57,8 +57,31 @@ constexpr ReplicaPlan<N, WAVES, RPW> plan_replicas() {
 // with r and r + 1: 64-70% of the row-form XORs for n = 20, 40, 64 (the first
 // level of the additive FFT of tools/xorgen/gen_encode_gm.py, without its
 // register-hungry deeper levels).
+// Horner steps acc * C + x with the constants of the split modes as Paar XOR
+// programs (tools/xorgen/gen_horner: shared pairs of acc planes between the
+// output rows), where that beats the row form; VDS_ENC_PAAR=0: row form only.
+#ifndef VDS_ENC_PAAR
+#define VDS_ENC_PAAR 1
+#endif
+template <uint32_t C>
+struct HornerPaar {
+  static constexpr int kCost = 0;  // 0: no program, the row form is used
+};
+#include "generated/horner_paar.inc"
+
+template <uint32_t C>
+__device__ __forceinline__ Plane16 plane_horner_enc(const Plane16 &acc, const Plane16 &x) {
+  if constexpr (VDS_ENC_PAAR && HornerPaar<C>::kCost > 0)
+    return HornerPaar<C>::apply(acc, x);
+  else
+    return plane_horner_rows<C>(acc, x);
+}
+constexpr int enc_step_cost(uint32_t c) {
+  return (VDS_ENC_PAAR && horner_paar_cost(c) > 0) ? horner_paar_cost(c) : horner_cost((int)c);
+}
+
 constexpr uint32_t pair_y(int r) { return gf16_mul((uint32_t)r, (uint32_t)r) ^ (uint32_t)r; }
-constexpr int pair_cost(int r) { return 2 * horner_cost((int)pair_y(r)) + 1; }
+constexpr int pair_cost(int r) { return 2 * enc_step_cost(pair_y(r)) + 1; }
 
 template <int WAVES, int PPW>
 struct PairPlan {
@@ -103,7 +126,7 @@ constexpr PairPlan<WAVES, PPW> plan_pairs() {
 constexpr uint32_t kQuadD = 6u;  // s(x) = x^2 + x
 constexpr uint32_t quad_z0(int j) { return gf16_mul(pair_y(4 * j), gf16_inv(kQuadD)); }
 constexpr uint32_t quad_w(int j) { return gf16_mul(quad_z0(j), quad_z0(j)) ^ quad_z0(j); }
-constexpr int quad_cost(int j) { return 4 * horner_cost((int)quad_w(j)) + 4; }
+constexpr int quad_cost(int j) { return 4 * enc_step_cost(quad_w(j)) + 4; }
 
 template <int WAVES, int QPW>
 struct QuadPlan {
@@ -376,8 +399,8 @@ __device__ __forceinline__ void encode_zero_dispatch(int wave, const FastEncodeA
 // In-place Taylor expansion at z^2 + z of c[OFF .. OFF + NN) (NN a power of
 // two): blocks C0..C3 of NN/4: C2 ^= C3, C1 ^= C2, then each half.  Cell 2i
 // ends as the coefficient i of P0, cell 2i + 1 as that of P1.
-template <int K, int OFF, int NN>
-__device__ __forceinline__ void taylor_inplace(u32x4 (&c)[K]) {
+template <int K, int OFF, int NN, class T>
+__device__ __forceinline__ void taylor_inplace(T (&c)[K]) {
   if constexpr (NN > 2) {
     constexpr int t = NN / 4;
 #pragma unroll
@@ -393,9 +416,28 @@ __device__ __forceinline__ void taylor_inplace(u32x4 (&c)[K]) {
 // parallel (the XORs never mix planes): wave w < 4 takes planes 4w..4w+3 of
 // every cell (one ds_read_b128 / ds_write_b128 per cell, conflict-free as
 // the Horner reads).
+#ifndef VDS_DIAG_ENC
+#define VDS_DIAG_ENC 0
+#endif
+// VDS_TAYLOR_WIDE: with 8 waves, each takes 2 planes (ds_read_b64) instead of
+// 4 waves taking 4 (A/B).
+#ifndef VDS_TAYLOR_WIDE
+#define VDS_TAYLOR_WIDE 0
+#endif
 template <int K, int N, int RPW, int WV>
 __device__ __forceinline__ void taylor_lds(int wave, uint32_t *set_planes) {
   using S = EncodeShape<K, N, RPW, WV>;
+  if constexpr (VDS_TAYLOR_WIDE && WV >= 8) {
+    if (wave < 8) {
+      u32x2 c[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) c[i] = *(lds_v2 *)(set_planes + S::cell_off(i) + 2 * wave);
+      taylor_inplace<K, 0, K>(c);
+#pragma unroll
+      for (int i = 0; i < K; ++i) *(lds_v2 *)(set_planes + S::cell_off(i) + 2 * wave) = c[i];
+    }
+    return;
+  }
   if (wave < 4) {
     u32x4 c[K];
 #pragma unroll
@@ -412,7 +454,7 @@ __device__ __forceinline__ void pair_step(Plane16 (&dst)[PP], const Plane16 (&sr
   using S = EncodeShape<K, N, RPW, WV>;
   [&]<size_t... I>(std::index_sequence<I...>) {
     constexpr auto r = [](int i) { return S0 + i < S::kPPW ? S::kPairs.r[W][S0 + i] : -1; };
-    ((r(I) >= 0 ? (void)(dst[I] = plane_horner_rows<(r(I) >= 0 ? pair_y(r(I)) : 0u)>(src[I], x)) : (void)0), ...);
+    ((r(I) >= 0 ? (void)(dst[I] = plane_horner_enc<(r(I) >= 0 ? pair_y(r(I)) : 0u)>(src[I], x)) : (void)0), ...);
   }(std::make_index_sequence<PP>{});
 }
 
@@ -558,11 +600,11 @@ __device__ __forceinline__ Plane16 quad_horner(const uint32_t *set_planes) {
 #pragma clang loop unroll(disable)
   for (int u = Q - 2; u >= 1; u -= 2) {
     const Plane16 xb = X(u - 1);
-    B = plane_horner_rows<W>(A, xa);
+    B = plane_horner_enc<W>(A, xa);
     xa = X(u - 2);
-    A = plane_horner_rows<W>(B, xb);
+    A = plane_horner_enc<W>(B, xb);
   }
-  return plane_horner_rows<W>(A, xa);
+  return plane_horner_enc<W>(A, xa);
 }
 
 template <int K, int N, int RPW, int WV, int W, bool ST, int S0 = 0>
@@ -782,9 +824,13 @@ void k_encode_bs(FastEncodeArgs a) {
       __syncthreads();
       quad_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
     } else if constexpr (SPLIT) {
+#if VDS_DIAG_ENC != 1  // diagnostic builds (wrong bytes, timing only): 1 = no Taylor step, 2 = no evaluation
       taylor_lds<K, N, RPW, WV>(wave, my_set);
       __syncthreads();
+#endif
+#if VDS_DIAG_ENC != 2
       pair_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
+#endif
     } else {
       encode_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
     }
@@ -795,16 +841,19 @@ void k_encode_bs(FastEncodeArgs a) {
 template <int K, int N, int RPW, int WV, bool STREAM, bool SPLIT, bool QUAD>
 static hipError_t launch_encode_bs_st(const FastEncodeArgs &a, hipStream_t s) {
   using S = EncodeShape<K, N, RPW, WV>;
-  hipError_t e = ensure_lds_attr(&k_encode_bs<K, N, RPW, WV, STREAM, SPLIT, QUAD>, S::kLdsBytes);
+  // VDS_EC_ENC_LDS_EXTRA: extra (unused) LDS bytes per workgroup, to measure
+  // the kernel at fewer workgroups per CU (diagnostic)
+  static const uint32_t extra = grid_override("VDS_EC_ENC_LDS_EXTRA");
+  const int lds = S::kLdsBytes + (int)(extra < 64 * 1024 ? extra : 0);
+  hipError_t e = ensure_lds_attr(&k_encode_bs<K, N, RPW, WV, STREAM, SPLIT, QUAD>, lds);
   if (e != hipSuccess) return e;
-  const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
+  const int blocks_per_cu = (160 * 1024) / lds;
   int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
   static const uint32_t over = grid_override("VDS_EC_ENC_GRID");
   if (over) grid = (int)over;
   if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_encode_bs<K, N, RPW, WV, STREAM, SPLIT, QUAD>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s,
-                     a);
+  hipLaunchKernelGGL((k_encode_bs<K, N, RPW, WV, STREAM, SPLIT, QUAD>), dim3(grid), dim3(S::kThreads), lds, s, a);
   return hipGetLastError();
 }
 

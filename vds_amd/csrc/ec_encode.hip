@@ -559,7 +559,7 @@ __device__ __forceinline__ void quad_twist_lds(int wave, uint32_t *set_planes) {
     if (wave == C % WV) {
       constexpr uint32_t tw = gf16_pow(kQuadD, (uint32_t)(C / 2));
       uint32_t *p = set_planes + S::cell_off(C);
-      const Plane16 v = plane_horner_rows<tw>(lds_planes(p), plane_zero());
+      const Plane16 v = plane_horner_enc<tw>(lds_planes(p), plane_zero());
 #pragma unroll
       for (int m = 0; m < 4; ++m)
         *(lds_v4 *)(p + 4 * m) = u32x4{v.p[4 * m], v.p[4 * m + 1], v.p[4 * m + 2], v.p[4 * m + 3]};
@@ -620,18 +620,18 @@ __device__ __forceinline__ void encode_quad_group(const uint32_t *set_planes, co
       {
         const Plane16 A1 = quad_horner<K, N, RPW, WV, w, 1>(set_planes);
         const Plane16 B1 = quad_horner<K, N, RPW, WV, w, 3>(set_planes);
-        p1y0 = plane_horner_rows<z0>(B1, A1);
+        p1y0 = plane_horner_enc<z0>(B1, A1);
         p1y1 = plane_xor(p1y0, B1);
       }
       const Plane16 A0 = quad_horner<K, N, RPW, WV, w, 0>(set_planes);
       const Plane16 B0 = quad_horner<K, N, RPW, WV, w, 2>(set_planes);
-      const Plane16 p0y0 = plane_horner_rows<z0>(B0, A0);
+      const Plane16 p0y0 = plane_horner_enc<z0>(B0, A0);
       const Plane16 p0y1 = plane_xor(p0y0, B0);
       __builtin_amdgcn_s_setprio(kEncStorePrio);
-      const Plane16 r0 = plane_horner_rows<(uint32_t)(4 * j)>(p1y0, p0y0);
+      const Plane16 r0 = plane_horner_enc<(uint32_t)(4 * j)>(p1y0, p0y0);
       store_rep<S::kMap, ST>(r0, rep_ptr(a, 4 * j), a, tp, lane, bm);
       store_rep<S::kMap, ST>(plane_xor(r0, p1y0), rep_ptr(a, 4 * j + 1), a, tp, lane, bm);
-      const Plane16 r2 = plane_horner_rows<(uint32_t)(4 * j + 2)>(p1y1, p0y1);
+      const Plane16 r2 = plane_horner_enc<(uint32_t)(4 * j + 2)>(p1y1, p0y1);
       store_rep<S::kMap, ST>(r2, rep_ptr(a, 4 * j + 2), a, tp, lane, bm);
       store_rep<S::kMap, ST>(plane_xor(r2, p1y1), rep_ptr(a, 4 * j + 3), a, tp, lane, bm);
       __builtin_amdgcn_s_setprio(0);

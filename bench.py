@@ -46,11 +46,15 @@ def parse():
     p.add_argument("--no-jit", action="store_true",
                    help="no run-time compiled survivor-set kernel: the repair runs k_restore_syn")
     p.add_argument("--live-objects", type=int, default=16384)
+    p.add_argument("--no-c4", action="store_true", help="skip the k=32, m=8 leg (BASELINE.json configs[3])")
+    p.add_argument("--c4-objects", type=int, default=1024, help="objects per GPU of the k=32, m=8 leg")
     p.add_argument("--replica-align", type=int, default=256,
                    help="replica buffers start on multiples of this many bytes (1: packed at the odd stride L)")
     p.add_argument("--cpu-objects", type=int, default=8, help="objects in the CPU baseline sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-object HBM bytes per kernel from rocprofv3 PMC passes (tools/pmc_traffic.py)")
+    p.add_argument("--traffic-json-k32", default=os.path.join(ROOT, "profiles", "traffic_k32.json"),
+                   help="the same for the k=32, n=40 kernels (the C4 leg)")
     return p.parse_args()
 
 
@@ -318,6 +322,121 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02
     return res
 
 
+def c4_jit_prebuild(k, nodes):
+    """Compile the C4 survivor set's kernel into the on-disk JIT cache on a
+    host thread while the headline runs (a k=32 compile takes ~12 s of host
+    CPU; no device is touched).  The leg's own warm-up then loads it from the
+    cache instead of waiting for a compile."""
+    import threading
+    import numpy as np
+    from vds_amd import _lib
+    nd = np.asarray(nodes, dtype=np.uint16)
+    th = threading.Thread(target=lambda: _lib.lib().vds_ec_jit_build16(k, nd.ctypes.data_as(_lib.u16p), None),
+                          daemon=True)
+    th.start()
+    return th
+
+
+def c4_leg(torch, chunk, dev, stream, args, rank, world, dist, prebuild=None):
+    """BASELINE.json configs[3]: k=32, m=8 encode of all 40 replicas and repair
+    from 32 (erased every fifth replica, {0, 5, .., 35}), objects round-robin
+    over the GPUs as the headline (weak scaling), 64 MiB objects, `--c4-objects`
+    per GPU (1024: 208 GiB of inputs, replicas and outputs).  Reported beside
+    the metric, never in it, with its own roofline block per kernel: algorithmic
+    bytes per launch (S + n L encode, k L + S repair) over the
+    HIP-event launch time, against 8 TB/s."""
+    k, m = 32, 8
+    n = k + m
+    size = 64 << 20
+    L = chunk.replica_size(k, size)
+    Ls = replica_stride(L, args.replica_align)
+    erased = list(range(0, n, n // m))[:m]
+    nodes = [r for r in range(n) if r not in erased][:k]
+    free, _total = torch.cuda.mem_get_info(dev)
+    per_obj = size + n * Ls + size
+    objects = min(args.c4_objects, max(1, int(0.92 * free // per_obj)))
+    if world > 1:
+        objects = int(-max_over_ranks([-objects], dist, dev)[0])
+    inp = torch.empty(objects * size, dtype=torch.uint8, device=dev)
+    reps = torch.empty((n, objects * Ls), dtype=torch.uint8, device=dev)
+    restored = torch.empty(objects * size, dtype=torch.uint8, device=dev)
+    for i, oid in enumerate(owned_objects(rank, world, objects)):
+        chunk.fill_splitmix_device(inp[i * size:], size, SEED ^ 0xC4 ^ (oid << 8))
+    rep_ptrs = [reps[i].data_ptr() for i in range(n)]
+    chunk_ptrs = [reps[r].data_ptr() for r in nodes]
+    padding = size % (2 * k)
+
+    def encode():
+        chunk.encode_device(k, list(range(n)), inp, size, size, objects, rep_ptrs, Ls)
+
+    def repair():
+        chunk.restore_device(k, nodes, chunk_ptrs, L, Ls, padding, objects, restored, size)
+
+    def timed(fn, steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        e0.record(stream)
+        for _ in range(steps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / steps
+
+    for _ in range(max(1, args.warmup)):
+        encode()
+    # the pattern-independent syndrome kernel first (it serves every set until
+    # the set's own kernel is loaded), then the survivor set's kernel
+    chunk.jit_set_mode(0)
+    repair()
+    aot_ms = timed(repair, args.steps)
+    aot_kernel = kernel_names(k, n, nodes, size, L, objects)[1]
+    jit_s = None
+    if not args.no_jit:
+        chunk.jit_set_mode(1)
+        t0 = time.perf_counter()
+        if prebuild is not None:
+            prebuild.join()
+        repair()
+        repair()
+        chunk.jit_wait()
+        repair()
+        jit_s = time.perf_counter() - t0
+    torch.cuda.synchronize(dev)
+    assert torch.equal(restored[:size], inp[:size]) and \
+        torch.equal(restored[(objects - 1) * size:], inp[(objects - 1) * size:]), "c4 repair differs"
+    enc_ms = timed(encode, args.steps)
+    rep_ms = timed(repair, args.steps)
+    if world > 1:
+        enc_ms, rep_ms, aot_ms = max_over_ranks([enc_ms, rep_ms, aot_ms], dist, dev)
+    sl = 1 << 30
+    assert all(torch.equal(restored[i:i + sl], inp[i:i + sl]) for i in range(0, objects * size, sl)), "c4 repair"
+    enc_name, rep_name = kernel_names(k, n, nodes, size, L, objects)
+    enc_bytes = objects * (size + n * L)
+    rep_bytes = objects * (k * L + size)
+    gb = world * objects * size / 2**30
+
+    def roof(name, nbytes, ms):
+        ach = nbytes / (ms * 1e-3) / 1e9
+        tr, src = pmc_traffic(args.traffic_json_k32, name, objects, k, n)
+        return {"kernel": name, "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(ms, 4),
+                "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": tr, "traffic_source": src}
+
+    res = {"workload": f"k={k},m={m} encode of all {n} replicas + repair from {k} (erased {erased}), "
+                       f"{objects} x 64 MiB objects per GPU",
+           "k": k, "m": m, "objects_per_gpu": objects, "n_gpus": world, "erased": erased,
+           "value": round(gb / ((enc_ms + rep_ms) * 1e-3), 3), "unit": "GiB/s",
+           "encode_GiBps": round(gb / (enc_ms * 1e-3), 3), "repair_GiBps": round(gb / (rep_ms * 1e-3), 3),
+           "encode_ms": round(enc_ms, 3), "repair_ms": round(rep_ms, 3),
+           "restore_aot_ms": round(aot_ms, 3), "restore_aot_kernel": aot_kernel,
+           "restore_kernel": rep_name, "jit_wait_s": round(jit_s, 3) if jit_s is not None else None,
+           "roofline": {"encode": roof(enc_name, enc_bytes, enc_ms), "repair": roof(rep_name, rep_bytes, rep_ms),
+                        "repair_aot": roof(aot_kernel, rep_bytes, aot_ms)}}
+    del inp, reps, restored
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -379,9 +498,29 @@ def main():
     def repair():
         chunk.restore_device(k, nodes, chunk_ptrs, L, Ls, padding, objects, restored, size)
 
+    c4_pre = None
+    if not args.no_c4 and not args.no_jit:
+        c4_pre = c4_jit_prebuild(32, [r for r in range(40) if r % 5][:32])
+    if not args.no_jit:
+        chunk.jit_set_mode(0)  # (the AOT timing below first)
     for _ in range(args.warmup):
         encode()
         repair()
+    # The pattern-independent syndrome kernel k_restore_syn serves a survivor
+    # set until the set's own kernel is loaded (every first-seen set, every
+    # deployment without the JIT helper): its repair time, beside the metric.
+    aot_ms = None
+    if not args.no_jit:
+        torch.cuda.synchronize(dev)
+        a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a0.record(stream)
+        for _ in range(args.steps):
+            repair()
+        a1.record(stream)
+        torch.cuda.synchronize(dev)
+        aot_ms = a0.elapsed_time(a1) / args.steps
+        aot_name = kernel_names(k, n, nodes, size, L, objects)[1]
+        chunk.jit_set_mode(1)
     # The survivor set's own restore kernel (vds_amd/csrc/vds_ec_jit.cpp) is
     # compiled in the background from the set's second use; a repair pass
     # keeps using it for the rest of the set's objects, so the steady state is
@@ -448,6 +587,8 @@ def main():
 
     if world > 1:
         elapsed, enc_ms, rep_ms = max_over_ranks([elapsed, enc_ms, rep_ms], dist, dev)
+        if aot_ms is not None:
+            aot_ms = max_over_ranks([aot_ms], dist, dev)[0]
 
     # Replica names, also beside the metric: SHA-256 of
     # every replica of the batch, one lane per replica (reps is [n][objects][L]).
@@ -521,12 +662,15 @@ def main():
                    "encode_ms": round(e16, 3), "repair_ms": round(r16, 3)}
         del reps16
 
+    if align16 is None:
+        del reps, digests, regen_out
+    del inp, restored
+    torch.cuda.empty_cache()
+    c4 = None
+    if not args.no_c4:
+        c4 = c4_leg(torch, chunk, dev, stream, args, rank, world, dist if world > 1 else None, c4_pre)
     live = None
     if not args.no_live:
-        if align16 is None:
-            del reps, digests, regen_out
-        del inp, restored
-        torch.cuda.empty_cache()
         live = live_shape(torch, chunk, dev, torch.cuda.Stream(dev), args.live_objects, args.steps, args.warmup,
                           align=args.replica_align)
 
@@ -559,6 +703,11 @@ def main():
                      "traffic_source": traffic_src, "algorithmic_bytes_per_launch": dom_bytes,
                      "avg_launch_ms": round(dom_ms, 4), "kernels": {"encode": enc_name, "repair": rep_name}},
         "restore_kernel": restore_kernel,
+        "restore_aot_ms": round(aot_ms, 3) if aot_ms is not None else None,
+        "restore_aot": ({"kernel": aot_name, "repair_GiBps": round(world * objects * size / (aot_ms * 1e-3) / 2**30, 3),
+                         "frac": round(rep_bytes / (aot_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+                        if aot_ms is not None else None),
+        "c4": c4,
         "jit_wait_s": round(jit_s, 3) if jit_s is not None else None,
         "align16": align16,
         "live_shape": live,

@@ -58,6 +58,10 @@ extern "C" {
 
 const char *vds_ec_strerror(int status);
 int vds_ec_version(void);
+/* Host staging contexts (pinned + device buffers and a stream per calling
+ * thread and device) created so far, and how many of them sit idle in the
+ * pool that exited threads return theirs to (diagnostics; host only).      */
+int vds_ec_host_ctx_stats(uint64_t *created, uint64_t *pooled);
 /* Number of HIP devices usable by the library (0 on a machine with none). */
 int vds_ec_device_count(int *count);
 

@@ -188,3 +188,78 @@ def test_batch_routes_mixed(gpu, k):
             g = x.cpu().numpy()
             assert np.array_equal(g[:csz[i]], O.encode(k, t, host)), (i, t)
             assert (g[csz[i]:] == 0x5A).all()
+
+
+def test_batch_many_threads_mixed_routes(gpu):
+    """More threads than the parameter ring has slots (16), each making
+    batched calls whose objects take both the syndrome and the RT route (two
+    slots per call), on streams of their own.  The two slots of a call are
+    reserved together, so no thread holds one while waiting for another (the
+    hold-and-wait deadlock of round 3).  Every output checked."""
+    import threading
+    import torch
+    from vds_amd import chunk
+    k, n = 16, 20
+    size = 2048 * 2 * k + 300
+    host = O.splitmix(SEED + 4242, size)
+    L = chunk.replica_size(k, size)
+    reps = {r: torch.from_numpy(O.encode(k, r, host)).cuda() for r in list(range(n)) + [40, 41, 42]}
+    sets = [list(range(k)), [r for r in range(n) if r not in (2, 9)][:k],  # syndrome route
+            list(range(2, k)) + [40, 41], list(range(1, k)) + [42]]        # RT route
+    nthreads, calls = 24, 6
+    outs = [[torch.zeros(size + 16, dtype=torch.uint8, device="cuda") for _ in sets] for _ in range(nthreads)]
+    errors = []
+    barrier = threading.Barrier(nthreads)
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream()
+            barrier.wait()
+            for _ in range(calls):
+                chunk.restore_batch_device(k, sets, [[reps[r].data_ptr() for r in nd] for nd in sets], [L] * len(sets),
+                                           [size % (2 * k)] * len(sets), [o.data_ptr() for o in outs[t]], stream=s)
+            s.synchronize()
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=90)
+    assert not any(x.is_alive() for x in th), "batched calls deadlocked"
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for t in range(nthreads):
+        for o in outs[t]:
+            got = o.cpu().numpy()
+            assert np.array_equal(got[:size], host)
+            assert (got[size:] == 0).all()
+
+
+def test_host_contexts_reused_across_threads(gpu):
+    """Each calling thread gets a host staging context (pinned and device
+    buffers and a stream); a thread that exits returns its context to a pool,
+    so short-lived threads reuse them instead of leaking one set each."""
+    import ctypes
+    import threading
+    from vds_amd import _lib, chunk
+    k = 16
+    data = O.splitmix(SEED + 77, 5000)
+    want = [O.encode(k, r, data) for r in range(4)]
+    created, pooled = ctypes.c_uint64(), ctypes.c_uint64()
+
+    def one():
+        got = chunk.encode_host(k, range(4), data)
+        assert all(np.array_equal(g, w) for g, w in zip(got, want))
+
+    one()  # this thread's own context
+    _lib.lib().vds_ec_host_ctx_stats(ctypes.byref(created), ctypes.byref(pooled))
+    before = created.value
+    for _ in range(12):  # sequential short-lived threads: one pooled context serves them all
+        t = threading.Thread(target=one)
+        t.start()
+        t.join()
+    _lib.lib().vds_ec_host_ctx_stats(ctypes.byref(created), ctypes.byref(pooled))
+    assert created.value <= before + 1, (before, created.value)
+    assert pooled.value >= 1

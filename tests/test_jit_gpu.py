@@ -54,8 +54,36 @@ def test_jit_disk_cache_across_processes(vds_lib, tmp_path):
                                 capture_output=True, text=True, timeout=300).stdout.split()[-1])
              for _ in range(2)]
     files = list(tmp_path.glob("*.co"))
-    assert len(files) == 1 and sizes[0] == sizes[1] == files[0].stat().st_size > 10000
-    assert not list(tmp_path.glob("*.tmp"))
+    # the file: a 32-byte header (magic, key, length, checksum), then the code object
+    assert len(files) == 1 and sizes[0] == sizes[1] == files[0].stat().st_size - 32 > 10000
+    head = files[0].read_bytes()[:32]
+    assert head[:8] == b"VDSECJ1\0" and int.from_bytes(head[16:24], "little") == sizes[0]
+    assert not list(tmp_path.glob("*.co.*"))  # (mkstemp temporaries renamed or removed)
+
+
+def test_jit_disk_cache_rejects_damaged_files(vds_lib, tmp_path):
+    """A cache file whose checksum, length or key does not match is a miss:
+    it is removed and the kernel recompiled (the directory may be shared)."""
+    import os
+    import subprocess
+    import sys
+    script = ("from vds_amd import chunk, _lib; _lib.lib();"
+              "print(chunk.jit_build(16, [r for r in range(20) if r not in (1, 6, 11, 16)]))")
+    env = dict(os.environ, VDS_EC_JIT_CACHE=str(tmp_path))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run():
+        return int(subprocess.run([sys.executable, "-c", script], env=env, cwd=root, check=True,
+                                  capture_output=True, text=True, timeout=300).stdout.split()[-1])
+    size = run()
+    f, = tmp_path.glob("*.co")
+    good = f.read_bytes()
+    for bad in (good[:-100],                                   # short
+                good[:5000] + bytes([good[5000] ^ 1]) + good[5001:],  # one flipped bit
+                b"\0" * len(good)):                            # foreign
+        f.write_bytes(bad)
+        assert run() == size
+        assert f.read_bytes() == good  # recompiled and rewritten
 
 
 @pytest.fixture

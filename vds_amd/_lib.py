@@ -34,6 +34,7 @@ vpp = C.POINTER(C.c_void_p)
 SIGNATURES = {
     "vds_ec_strerror": (C.c_char_p, [C.c_int]),
     "vds_ec_version": (C.c_int, []),
+    "vds_ec_host_ctx_stats": (C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "vds_ec_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "vds_ec_replica_size": (C.c_uint64, [C.c_uint, C.c_uint, C.c_uint64, C.c_uint]),
     "vds_ec_restored_size": (C.c_uint64, [C.c_uint, C.c_uint, C.c_uint64, C.c_uint16]),

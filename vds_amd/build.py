@@ -38,6 +38,12 @@ JIT_FILES = ["gf_common.hpp", "bitslice.hpp", "ec_internal.hpp", "ec_device.hpp"
 ARCH = os.environ.get("VDS_EC_ARCH", "gfx950")
 
 
+def _arch_define() -> str:
+    """The target architecture, for the JIT helper (its --offload-arch) and the
+    library (the JIT cache key): both must agree with the library's own."""
+    return f'-DVDS_EC_ARCH_STR="{ARCH}"'
+
+
 def _hipcc() -> str:
     for c in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if c and os.path.exists(c):
@@ -76,7 +82,7 @@ def write_jit_embed(out_dir: str) -> None:
 
 
 def compile_cmd(src: str, obj: str, defines: tuple[str, ...] = (), includes: tuple[str, ...] = ()) -> list[str]:
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-c", *defines,
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-c", *defines, _arch_define(),
            "-I", os.path.join(ROOT, "include"), *[a for d in includes for a in ("-I", d)],
            os.path.join(CSRC, src), "-o", obj]
     if src.endswith(".cpp"):
@@ -95,7 +101,7 @@ def _compile_all(tmp: str, defines: tuple[str, ...], verbose: bool) -> list[str]
         jobs.append((cmd, obj))
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 1), 8))
     rocm = os.path.dirname(os.path.dirname(os.path.realpath(_hipcc())))
-    jitc = [_hipcc(), "-O2", "-std=c++20", "-I", tmp, os.path.join(CSRC, "vds_ec_jitc.cpp"), "-o",
+    jitc = [_hipcc(), "-O2", "-std=c++20", _arch_define(), "-I", tmp, os.path.join(CSRC, "vds_ec_jitc.cpp"), "-o",
             os.path.join(tmp, "vds_ec_jitc"), f"-L{rocm}/lib", "-lhiprtc", f"-Wl,-rpath,{rocm}/lib",
             "-Wl,--disable-new-dtags"]
     with cf.ThreadPoolExecutor(workers) as ex:

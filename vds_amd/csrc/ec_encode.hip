@@ -425,25 +425,9 @@ __device__ __forceinline__ void taylor_inplace(T (&c)[K]) {
 #ifndef VDS_DIAG_ENC
 #define VDS_DIAG_ENC 0
 #endif
-// VDS_TAYLOR_WIDE: with 8 waves, each takes 2 planes (ds_read_b64) instead of
-// 4 waves taking 4 (A/B).
-#ifndef VDS_TAYLOR_WIDE
-#define VDS_TAYLOR_WIDE 0
-#endif
 template <int K, int N, int RPW, int WV>
 __device__ __forceinline__ void taylor_lds(int wave, uint32_t *set_planes) {
   using S = EncodeShape<K, N, RPW, WV>;
-  if constexpr (VDS_TAYLOR_WIDE && WV >= 8) {
-    if (wave < 8) {
-      u32x2 c[K];
-#pragma unroll
-      for (int i = 0; i < K; ++i) c[i] = *(lds_v2 *)(set_planes + S::cell_off(i) + 2 * wave);
-      taylor_inplace<K, 0, K>(c);
-#pragma unroll
-      for (int i = 0; i < K; ++i) *(lds_v2 *)(set_planes + S::cell_off(i) + 2 * wave) = c[i];
-    }
-    return;
-  }
   if (wave < 4) {
     u32x4 c[K];
 #pragma unroll
@@ -737,27 +721,6 @@ __device__ __forceinline__ void encode_unpack16(const u32x4 (&V)[16], uint32_t (
   }
 }
 
-// Which wave evaluates which replicas (A/B, VDS_ENC_WAVE_ROT): the plans give
-// some waves one pair / quad more than others; two workgroups per CU place
-// their waves on the SIMDs alike, so the heavy waves may share SIMDs.
-// 1: rotate the assignment by the workgroup's index within its XCD; 2: half
-// a turn for every other one; 3: reversed for every other one.
-#ifndef VDS_ENC_WAVE_ROT
-#define VDS_ENC_WAVE_ROT 0
-#endif
-template <int WV>
-__device__ __forceinline__ int eval_wave(int wave) {
-  const int b = (int)(blockIdx.x >> 3);
-  if constexpr (VDS_ENC_WAVE_ROT == 1)
-    return (wave + b) & (WV - 1);
-  else if constexpr (VDS_ENC_WAVE_ROT == 2)
-    return (wave + (b & 1) * (WV / 2)) & (WV - 1);
-  else if constexpr (VDS_ENC_WAVE_ROT == 3)
-    return (b & 1) ? WV - 1 - wave : wave;
-  else
-    return wave;
-}
-
 // STREAM: tiles may straddle objects (groups_per_obj % 16 != 0, k >= 8); the
 // non-stream instantiation keeps one base address per tile.  SPLIT: replica
 // pairs from the one-level split (Taylor coefficients in LDS); QUAD (with
@@ -769,7 +732,6 @@ void k_encode_bs(FastEncodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ewave = eval_wave<WV>(wave);
   // transposes: this lane's set and 4-cell group; Horner: lane = set
   const int tset = wave * S::kSetsPerWave + lane / S::kLanesPerSet;
   const int tp = lane % S::kLanesPerSet;
@@ -805,11 +767,11 @@ void k_encode_bs(FastEncodeArgs a) {
     // its first tile, which that tile overwrites, in order, from the same
     // wave) makes both states alike.
     if constexpr (QUAD)
-      quad_zero_dispatch<K, N, RPW, WV, STREAM, 0>(ewave, a, tile_pos(a, tile), lane, bm);
+      quad_zero_dispatch<K, N, RPW, WV, STREAM, 0>(wave, a, tile_pos(a, tile), lane, bm);
     else if constexpr (SPLIT)
-      pair_zero_dispatch<K, N, RPW, WV, STREAM, 0>(ewave, a, tile_pos(a, tile), lane, bm);
+      pair_zero_dispatch<K, N, RPW, WV, STREAM, 0>(wave, a, tile_pos(a, tile), lane, bm);
     else
-      encode_zero_dispatch<K, N, RPW, WV, STREAM, 0>(ewave, a, tile_pos(a, tile), lane, bm);
+      encode_zero_dispatch<K, N, RPW, WV, STREAM, 0>(wave, a, tile_pos(a, tile), lane, bm);
   }
   for (; tile < t_end; tile += t_step) {
     // ---- transpose to planes and publish in LDS: cell 4p+2g+h, bit b = R[g][16h + (b^8)]
@@ -854,17 +816,17 @@ void k_encode_bs(FastEncodeArgs a) {
       __syncthreads();
       quad_taylor_lds<K, N, RPW, WV>(wave, my_set);
       __syncthreads();
-      quad_dispatch<K, N, RPW, WV, STREAM, 0>(ewave, my_set, a, tile_pos(a, tile), lane, bm);
+      quad_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
     } else if constexpr (SPLIT) {
 #if VDS_DIAG_ENC != 1  // diagnostic builds (wrong bytes, timing only): 1 = no Taylor step, 2 = no evaluation
       taylor_lds<K, N, RPW, WV>(wave, my_set);
       __syncthreads();
 #endif
 #if VDS_DIAG_ENC != 2
-      pair_dispatch<K, N, RPW, WV, STREAM, 0>(ewave, my_set, a, tile_pos(a, tile), lane, bm);
+      pair_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
 #endif
     } else {
-      encode_dispatch<K, N, RPW, WV, STREAM, 0>(ewave, my_set, a, tile_pos(a, tile), lane, bm);
+      encode_dispatch<K, N, RPW, WV, STREAM, 0>(wave, my_set, a, tile_pos(a, tile), lane, bm);
     }
     __syncthreads();
   }

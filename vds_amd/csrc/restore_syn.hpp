@@ -247,10 +247,6 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
 #ifndef VDS_GM2_PRIO
 #define VDS_GM2_PRIO 9
 #endif
-// The survivor-set kernel's scatter fill at wave priority 1 (A/B).
-#ifndef VDS_FILL_PRIO
-#define VDS_FILL_PRIO 0
-#endif
 template <int K, int N, int WV, int W>
 __device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
   using P = RestorePrograms<K, N, WV>;
@@ -375,37 +371,18 @@ __device__ __forceinline__ void rec_dual(Plane16 &acc, const Plane16 &t, const P
 // LDS XOR of a point's sixteen planes (this lane's 64 bytes) as eight
 // ds_xor_b64: planes 4g..4g+3 of point pt at byte (4 pt + g) 1 KiB + 16 lane.
 // With every lane on the same 8-byte half of its 16-byte slot, lanes 8 or 16
-// apart hit the same banks (2-way: +512 conflict cycles per tile in the
-// survivor-set kernel, round 3).  VDS_LDS_XOR_SWZ=1: a lane whose bits 3 and
-// 4 differ takes the other half first (distinct banks per 16- and 32-lane
-// group; the data follows with v_cndmask).  It removed every conflict
+// apart hit the same banks (2-way).  A swizzle that gave lanes whose bits 3
+// and 4 differ the other half first removed every conflict
 // (SQ_LDS_BANK_CONFLICT 0) and was slower: same box, k = 16 repair 13.99-
-// 14.04 -> 14.17-14.33 ms with the split copy-out reads below, k = 32 9.67 ->
-// 10.41 ms (profiles/round3/ab/swz_ab.log).  Off by default.
-#ifndef VDS_LDS_XOR_SWZ
-#define VDS_LDS_XOR_SWZ 0
-#endif
-#ifndef VDS_COPYOUT_VOLATILE  // (k = 16 copy-out reads: see the staging below; volatile = two ds_read_b64, A/B)
-#define VDS_COPYOUT_VOLATILE
-#endif
+// 14.04 -> 14.17-14.33 ms, k = 32 9.67 -> 10.41 ms
+// (profiles/round3/ab/swz_ab.log; deleted in round 4).
 __device__ __forceinline__ void lds_xor_point(const SynLds &L, int pt, const Plane16 &v) {
   __attribute__((address_space(3))) uint64_t *dst =
       (__attribute__((address_space(3))) uint64_t *)(L.base + L.lo + 4096u * pt);
-  if constexpr (VDS_LDS_XOR_SWZ != 0) {
-    const uint32_t sw = ((L.lo >> 7) ^ (L.lo >> 8)) & 1u;  // bit 3 ^ bit 4 of the lane (L.lo = 16 lane)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const uint64_t a = (uint64_t)v.p[4 * g] | ((uint64_t)v.p[4 * g + 1] << 32);
-      const uint64_t b = (uint64_t)v.p[4 * g + 2] | ((uint64_t)v.p[4 * g + 3] << 32);
-      __hip_atomic_fetch_xor(dst + 128 * g + sw, sw ? b : a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_xor(dst + 128 * g + (sw ^ 1u), sw ? a : b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  } else {
-#pragma unroll
-    for (int h = 0; h < 8; ++h)
-      __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1), (uint64_t)v.p[2 * h] | ((uint64_t)v.p[2 * h + 1] << 32),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
+  for (int h = 0; h < 8; ++h)
+    __hip_atomic_fetch_xor(dst + 128 * (h >> 1) + (h & 1), (uint64_t)v.p[2 * h] | ((uint64_t)v.p[2 * h + 1] << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Scatter fill (FillP::kScatter, vds_ec_jit.cpp): wave W's share of every
@@ -756,9 +733,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     } else if constexpr (kScatter) {
       // ---- 2''. this wave's survivors' share of every erased point below K
       // (its own stage-1 slots in, LDS XOR atomics out; survivors sorted by point)
-      syn_prio<1, kPrio && (VDS_FILL_PRIO != 0)>();
       syn_scatter_fill<WV, FillP, 0>(wave, L);
-      syn_prio<0, kPrio && (VDS_FILL_PRIO != 0)>();
       if (!kLateLoad) prefetch(tile + t_step);
     } else if constexpr (FILL) {
       if (wave < FillP::kFill) {
@@ -958,11 +933,11 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
         // (the compiler merges the two halves into one ds_read2_b64: 8 LDS
         // cycles, banks (a/4) mod 32 over 16 lanes, 2-way at lanes l, l + 8;
         // as two volatile ds_read_b64 -- 2 + 2 cycles, conflict-free thanks to
-        // the padding -- they measured slower, VDS_COPYOUT_VOLATILE)
+        // the padding -- they measured slower, swz_ab.log)
         auto piece = [&](int i) {
           const lds_char *r = r0 + 1056 * i;
-          const u32x2 v0 = *(__attribute__((address_space(3))) const VDS_COPYOUT_VOLATILE u32x2 *)r;
-          const u32x2 v1 = *(__attribute__((address_space(3))) const VDS_COPYOUT_VOLATILE u32x2 *)(r + 8);
+          const u32x2 v0 = *(__attribute__((address_space(3))) const u32x2 *)r;
+          const u32x2 v1 = *(__attribute__((address_space(3))) const u32x2 *)(r + 8);
           return u32x4{v0[0], v0[1], v1[0], v1[1]};
         };
         if (!guard) {

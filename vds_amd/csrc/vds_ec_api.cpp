@@ -331,60 +331,80 @@ ParamRing *param_ring() {
   return rings[dev];
 }
 
-// A slot of at least `bytes` whose host side the caller may write (sl->h);
-// then param_commit copies it to the device on the caller's stream, and
-// param_release after the launches reading it.  A slot stays reserved
-// (busy) from acquire to release, so threads sharing the ring never write
-// one another's.
-hipError_t param_acquire(size_t bytes, ParamSlot **out) {
-  *out = nullptr;
+// `cnt` slots of at least bytes[i] each, whose host sides the caller may
+// write (out[i]->h); then param_commit copies one to the device on the
+// caller's stream, and param_release after the launches reading it.  A slot
+// stays reserved (busy) from acquire to release, so threads sharing the ring
+// never write one another's.  The cnt slots are reserved together, under one
+// hold of the ring's lock: a caller never holds a slot while it waits for
+// another (two batch builders each holding one of the last slots and waiting
+// for a second would deadlock), so with cnt <= 2 < kSlots every waiter is
+// eventually served.
+hipError_t param_acquire_n(int cnt, const size_t *bytes, ParamSlot **out) {
+  for (int i = 0; i < cnt; ++i) out[i] = nullptr;
+  if (cnt <= 0) return hipSuccess;
   ParamRing *r = param_ring();
   if (!r) return hipErrorNoDevice;
+  if (cnt > ParamRing::kSlots / 2) return hipErrorInvalidValue;
   std::unique_lock<std::mutex> g(r->mu);
   hipError_t e = hipSuccess;
   if (!r->copy && (e = hipStreamCreateWithFlags(&r->copy, hipStreamNonBlocking)) != hipSuccess) return e;
-  // first choice: an idle slot already big enough whose readers are done
-  // (no allocation, no wait); else the next idle slot in rotation; with all
-  // kSlots reserved by other threads, wait for a release
-  ParamSlot *sp = nullptr;
+  // per slot, first choice: an idle slot already big enough whose readers are
+  // done (no allocation, no wait); else the next idle slot in rotation; with
+  // fewer than cnt idle slots, take none and wait for a release
+  ParamSlot *sp[ParamRing::kSlots / 2] = {};
+  bool pending[ParamRing::kSlots / 2] = {};
   for (;;) {
-    for (int i = 0; i < ParamRing::kSlots && !sp; ++i) {
-      ParamSlot &c = r->slot[(r->next + i) % ParamRing::kSlots];
-      if (!c.busy && c.cap >= bytes && (!c.pending || hipEventQuery(c.ev) == hipSuccess)) sp = &c;
+    int got = 0;
+    for (; got < cnt; ++got) {
+      ParamSlot *p = nullptr;
+      for (int i = 0; i < ParamRing::kSlots && !p; ++i) {
+        ParamSlot &c = r->slot[(r->next + i) % ParamRing::kSlots];
+        if (!c.busy && c.cap >= bytes[got] && (!c.pending || hipEventQuery(c.ev) == hipSuccess)) p = &c;
+      }
+      for (int i = 0; i < ParamRing::kSlots && !p; ++i) {
+        ParamSlot &c = r->slot[r->next++ % ParamRing::kSlots];
+        if (!c.busy) p = &c;
+      }
+      if (!p) break;
+      p->busy = true;
+      sp[got] = p;
     }
-    for (int i = 0; i < ParamRing::kSlots && !sp; ++i) {
-      ParamSlot &c = r->slot[r->next++ % ParamRing::kSlots];
-      if (!c.busy) sp = &c;
-    }
-    if (sp) break;
+    if (got == cnt) break;
+    for (int i = 0; i < got; ++i) sp[i]->busy = false;  // (none held while waiting)
     r->freed.wait(g);
   }
-  ParamSlot &sl = *sp;
-  sl.busy = true;  // reserved: from here on only this thread touches it
-  const bool pending = sl.pending;
-  sl.pending = false;
-  g.unlock();  // (the event wait and any allocation run outside the ring's lock)
-  auto fail = [&](hipError_t err) {
-    std::lock_guard<std::mutex> g2(r->mu);
-    sl.busy = false;
-    r->freed.notify_one();
-    return err;
-  };
-  if (pending && (e = hipEventSynchronize(sl.ev)) != hipSuccess) return fail(e);
-  if (!sl.ev && (e = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming)) != hipSuccess) return fail(e);
-  if (!sl.copied && (e = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming)) != hipSuccess) return fail(e);
-  if (bytes > sl.cap) {
-    if (sl.h) (void)hipHostFree(sl.h);
-    if (sl.d) (void)hipFree(sl.d);
-    sl.h = sl.d = nullptr;
-    sl.cap = 0;
-    if ((e = hipHostMalloc(&sl.h, bytes, 0)) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&sl.d, bytes)) != hipSuccess) return fail(e);
-    sl.cap = bytes;
+  for (int i = 0; i < cnt; ++i) {  // reserved: from here on only this thread touches them
+    pending[i] = sp[i]->pending;
+    sp[i]->pending = false;
   }
-  *out = &sl;
+  g.unlock();  // (the event waits and any allocation run outside the ring's lock)
+  for (int i = 0; i < cnt && e == hipSuccess; ++i) {
+    ParamSlot &sl = *sp[i];
+    if (pending[i]) e = hipEventSynchronize(sl.ev);
+    if (e == hipSuccess && !sl.ev) e = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming);
+    if (e == hipSuccess && !sl.copied) e = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming);
+    if (e == hipSuccess && bytes[i] > sl.cap) {
+      if (sl.h) (void)hipHostFree(sl.h);
+      if (sl.d) (void)hipFree(sl.d);
+      sl.h = sl.d = nullptr;
+      sl.cap = 0;
+      e = hipHostMalloc(&sl.h, bytes[i], 0);
+      if (e == hipSuccess) e = hipMalloc(&sl.d, bytes[i]);
+      if (e == hipSuccess) sl.cap = bytes[i];
+    }
+  }
+  if (e != hipSuccess) {  // all of them back, unused (nothing was enqueued on them)
+    std::lock_guard<std::mutex> g2(r->mu);
+    for (int i = 0; i < cnt; ++i) sp[i]->busy = false;
+    r->freed.notify_all();
+    return e;
+  }
+  for (int i = 0; i < cnt; ++i) out[i] = sp[i];
   return hipSuccess;
 }
+
+hipError_t param_acquire(size_t bytes, ParamSlot **out) { return param_acquire_n(1, &bytes, out); }
 
 // The copy runs on the ring's copy stream and s waits for it, so the copy
 // for one call overlaps the kernels of the call before it on s.  (The slot's
@@ -406,7 +426,7 @@ hipError_t param_release(ParamSlot *sl, hipStream_t s) {
   const hipError_t e = hipEventRecord(sl->ev, s);
   sl->pending = e == hipSuccess;
   sl->busy = false;
-  r->freed.notify_one();
+  r->freed.notify_all();  // (waiters need one or two slots: each re-checks)
   return e;
 }
 
@@ -677,9 +697,13 @@ void parallel_copy(const std::vector<Copy> &parts_in) {
 }
 
 // --------------------------------------------------------- host staging
-// Per (thread, device) staging context.  Contexts are never destroyed: they
-// live until process exit, when the HIP runtime reclaims them (freeing them
-// from a thread_local destructor would race the runtime's own teardown).
+// Per (thread, device) staging context.  When a thread exits, its contexts go
+// back to a process-wide pool, from which the next thread that needs one on
+// that device takes it: short-lived caller threads reuse the pinned and
+// device buffers instead of leaking a set each.  (Nothing is freed in the
+// thread-exit hook: at process exit it would race the HIP runtime's own
+// teardown.  Every host entry point waits for its stream before returning, so
+// a pooled context has no work in flight.)
 struct HostCtx {
   hipStream_t stream = nullptr;
   uint8_t *d_in = nullptr;
@@ -762,13 +786,55 @@ struct HostCtx {
   }
 };
 
+std::atomic<uint64_t> g_host_ctx_created{0};
+struct HostCtxPool {
+  std::mutex mu;
+  std::vector<std::vector<HostCtx *>> idle;  // per device
+};
+HostCtxPool &host_ctx_pool() {
+  static HostCtxPool *p = new HostCtxPool();  // never freed: outlives every thread
+  return *p;
+}
+struct HostCtxOwner {  // a thread's contexts; back to the pool at thread exit
+  std::vector<HostCtx *> per_device;
+  ~HostCtxOwner() {
+    HostCtxPool &p = host_ctx_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    for (size_t d = 0; d < per_device.size(); ++d) {
+      if (!per_device[d]) continue;
+      per_device[d]->win_valid = false;  // (the replica window belongs to this thread's calls)
+      if (p.idle.size() <= d) p.idle.resize(d + 1);
+      p.idle[d].push_back(per_device[d]);
+    }
+  }
+};
+
 HostCtx *host_ctx() {
-  thread_local std::vector<HostCtx *> per_device;
+  thread_local HostCtxOwner own;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
-  if ((size_t)dev >= per_device.size()) per_device.resize(dev + 1, nullptr);
-  if (!per_device[dev]) per_device[dev] = new HostCtx();
-  return per_device[dev];
+  if ((size_t)dev >= own.per_device.size()) own.per_device.resize(dev + 1, nullptr);
+  if (!own.per_device[dev]) {
+    HostCtxPool &p = host_ctx_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    if ((size_t)dev < p.idle.size() && !p.idle[dev].empty()) {
+      own.per_device[dev] = p.idle[dev].back();
+      p.idle[dev].pop_back();
+    } else {
+      own.per_device[dev] = new HostCtx();
+      g_host_ctx_created.fetch_add(1, std::memory_order_relaxed);
+    }
+  }
+  return own.per_device[dev];
+}
+
+// Contexts created and pooled so far (vds_ec_host_ctx_stats).
+size_t host_ctx_pooled() {
+  HostCtxPool &p = host_ctx_pool();
+  std::lock_guard<std::mutex> g(p.mu);
+  size_t n = 0;
+  for (const auto &v : p.idle) n += v.size();
+  return n;
 }
 
 // Host-buffer encode.  The drop-in chunk_generator<T>::write encodes one
@@ -1372,15 +1438,20 @@ struct SynBatchBuild {
 
   static size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
 
-  hipError_t begin(uint32_t count, uint64_t halves) {
+  // The slot bytes for `count` objects of `halves` half tiles; then attach().
+  size_t layout(uint32_t count, uint64_t halves) {
     nobj = count;
     cap_objs = (size_t)count + 1;
     cap_tiles = (size_t)((halves + count + 1) / 2 + 1);  // pairs within each plan: <= (halves + plans) / 2
     cap_plans = count;
     o_tiles = up16(cap_objs * sizeof(SynBatchObj));
     o_plans = up16(o_tiles + cap_tiles * sizeof(SynBatchTile));
-    hipError_t e = param_acquire(o_plans + cap_plans * sizeof(SynBatchPlan), &slot);
-    if (e == hipSuccess) objs = reinterpret_cast<SynBatchObj *>(slot->h);
+    return o_plans + cap_plans * sizeof(SynBatchPlan);
+  }
+  void attach(ParamSlot *sl) {
+    slot = sl;
+    objs = reinterpret_cast<SynBatchObj *>(slot->h);
+    const uint32_t count = nobj;
     obj_plan.assign(count, 0);
     obj_halves.assign(count, 0);
     unsigned bits = 4;
@@ -1388,7 +1459,6 @@ struct SynBatchBuild {
     hkey.assign(1ull << bits, 0);
     hval.assign(1ull << bits, 0);
     hshift = 64 - bits;
-    return e;
   }
   // The plan of survivor set `seen` (UINT32_MAX: no solve; not for distinct points).
   uint32_t plan_of(uint64_t seen) {
@@ -1490,16 +1560,20 @@ struct RtBatchBuild {
 
   static size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
 
-  hipError_t begin(uint32_t count, uint64_t halves, uint64_t rows) {
+  // The slot bytes for `count` descriptors of `halves` half tiles and `rows`
+  // coefficient rows; then attach().
+  size_t layout(uint32_t count, uint64_t halves, uint64_t rows) {
     nobj = count;
     cap_tiles = (size_t)(halves + 1) / 2 + 1;
     cap_rows = rows;
     o_tiles = up16(((size_t)count + 1) * sizeof(SynBatchObj));
     o_coef = up16(o_tiles + cap_tiles * sizeof(SynBatchTile));
-    hipError_t e = param_acquire(o_coef + cap_rows * k * sizeof(uint16_t) + 16, &slot);
-    if (e == hipSuccess) objs = reinterpret_cast<SynBatchObj *>(slot->h);
-    obj_halves.assign(count, 0);
-    return e;
+    return o_coef + cap_rows * k * sizeof(uint16_t) + 16;
+  }
+  void attach(ParamSlot *sl) {
+    slot = sl;
+    objs = reinterpret_cast<SynBatchObj *>(slot->h);
+    obj_halves.assign(nobj, 0);
   }
   // Descriptor i of survivors nd (chunks ch; ids < 256), rows at the points
   // rowp[0..ne) stored from row `row0` of the slot's coefficient area: slot a
@@ -1612,26 +1686,28 @@ struct BatchIndex {
   }
 };
 
-// Resolve the syndrome objects' plans (serial: the plan store and the
-// per-call hash), acquire both builders' slots.
+// Acquire both builders' slots (together: see param_acquire_n), resolve the
+// syndrome objects' plans (serial: the plan store and the per-call hash).
 int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, SynBatchBuild &bb, RtBatchBuild &rb,
                 std::vector<uint32_t> &plan, hipStream_t s) {
+  size_t bytes[2];
+  ParamSlot *sl[2] = {};
+  int nb = 0;
+  if (ix.nsyn) bytes[nb++] = bb.layout(ix.nsyn, ix.syn_halves);
+  if (ix.nrt) bytes[nb++] = rb.layout(ix.nrt, ix.rt_halves, ix.rt_rows);
+  const hipError_t e = param_acquire_n(nb, bytes, sl);
+  if (e != hipSuccess) return hip_status(e);
+  nb = 0;
+  if (ix.nsyn) bb.attach(sl[nb++]);
+  if (ix.nrt) rb.attach(sl[nb++]);
   if (ix.nsyn) {
-    hipError_t e = bb.begin(ix.nsyn, ix.syn_halves);
-    if (e != hipSuccess) return hip_status(e);
     plan.assign(info.size(), 0);
     for (uint32_t o = 0; o < info.size(); ++o)
       if (info[o].route == kRouteSyn && (plan[o] = bb.plan_of(info[o].seen)) == UINT32_MAX) {
         bb.abandon(s);
+        if (ix.nrt) rb.abandon(s);
         return VDS_EC_ESINGULAR;
       }
-  }
-  if (ix.nrt) {
-    hipError_t e = rb.begin(ix.nrt, ix.rt_halves, ix.rt_rows);
-    if (e != hipSuccess) {
-      if (ix.nsyn) bb.abandon(s);
-      return hip_status(e);
-    }
   }
   return VDS_EC_OK;
 }
@@ -2254,6 +2330,12 @@ const char *vds_ec_strerror(int status) {
 }
 
 int vds_ec_version(void) { return kVersion; }
+
+int vds_ec_host_ctx_stats(uint64_t *created, uint64_t *pooled) {
+  if (created) *created = g_host_ctx_created.load(std::memory_order_relaxed);
+  if (pooled) *pooled = host_ctx_pooled();
+  return VDS_EC_OK;
+}
 
 int vds_ec_device_count(int *count) {
   if (!count) return VDS_EC_EINVAL;

@@ -49,20 +49,12 @@ extern char **environ;
 #ifndef VDS_GM2
 #define VDS_GM2 1  // (restore_syn.hpp's defaults)
 #endif
-#ifndef VDS_LDS_XOR_SWZ
-#define VDS_LDS_XOR_SWZ 0
-#endif
 #ifndef VDS_GM2_PRIO
 #define VDS_GM2_PRIO 9
 #endif
-#ifndef VDS_FILL_PRIO
-#define VDS_FILL_PRIO 0
+#ifndef VDS_EC_ARCH_STR
+#define VDS_EC_ARCH_STR "gfx950"  // (build.py passes the library's architecture)
 #endif
-#ifndef VDS_COPYOUT_VOLATILE
-#define VDS_COPYOUT_VOLATILE
-#endif
-#define VDS_STR2(x) #x
-#define VDS_STR(x) VDS_STR2(x)
 
 namespace vds_ec {
 namespace {
@@ -126,11 +118,13 @@ struct Key {
 
 struct Entry {
   enum State { kPending, kReady, kFailed };
-  State state = kPending;
+  State state = kPending;  // (Jit::mu_)
   std::vector<char> code;
   std::string log;
-  hipModule_t mod[kJitMaxDev] = {};
-  hipFunction_t fn[kJitMaxDev] = {};
+  std::string cache_file;  // where `code` came from or went (removed if it fails to load)
+  hipModule_t mod[kJitMaxDev] = {};  // (Jit::load_mu_)
+  // published with release once loaded; read with acquire without load_mu_
+  std::atomic<hipFunction_t> fn[kJitMaxDev] = {};
 };
 
 // The kernel source for one survivor set.
@@ -141,10 +135,8 @@ std::string kernel_source(const Key &key) {
     if ((key.survivors >> a) & 1u) sp.push_back(a);
   std::string s;
   xorgen::appendf(s,
-                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n#define VDS_FILL_PRIO %d\n#define VDS_LDS_XOR_SWZ %d\n"
-                  "#define VDS_COPYOUT_VOLATILE %s\n",
-                  VDS_GM2, VDS_GM2_PRIO, VDS_FILL_PRIO, VDS_LDS_XOR_SWZ,
-                  VDS_STR(VDS_COPYOUT_VOLATILE));  // (the forms this library was built with)
+                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n", VDS_GM2,
+                  VDS_GM2_PRIO);  // (the forms this library was built with)
   xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
   xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
   if (key.regen) {  // every erased point, in ascending order (= SynRestoreArgs::erased)
@@ -223,36 +215,90 @@ uint64_t fnv1a(const void *p, size_t n, uint64_t h = 1469598103934665603ull) {
   return h;
 }
 
-std::string cache_path(const std::string &src, const std::string &helper) {
-  const std::string dir = cache_dir();
-  if (dir.empty()) return {};
+// The cache key: the kernel source, the target architecture and the helper's
+// size and mtime.
+uint64_t cache_key(const std::string &src, const std::string &helper) {
   struct stat st {};
-  if (stat(helper.c_str(), &st) != 0) return {};
+  if (stat(helper.c_str(), &st) != 0) return 0;
   uint64_t h = fnv1a(src.data(), src.size());
+  h = fnv1a(VDS_EC_ARCH_STR, sizeof VDS_EC_ARCH_STR, h);
   const int64_t id[2] = {(int64_t)st.st_size, (int64_t)st.st_mtime};
-  h = fnv1a(id, sizeof id, h);
+  return fnv1a(id, sizeof id, h) | 1u;  // (0: no key)
+}
+
+std::string cache_path(uint64_t key) {
+  const std::string dir = cache_dir();
+  if (dir.empty() || key == 0) return {};
   char name[64];
-  std::snprintf(name, sizeof name, "/%016llx.co", (unsigned long long)h);
+  std::snprintf(name, sizeof name, "/%016llx.co", (unsigned long long)key);
   return dir + name;
+}
+
+// A cache file is this header, then the code object.  A file whose header
+// does not match (another key, a short or foreign file, damaged bytes) is a
+// miss, and is removed: the cache directory may be shared, so nothing in it
+// is trusted until its key, length and checksum agree.
+struct CacheHeader {
+  char magic[8];   // "VDSECJ1"
+  uint64_t key;    // cache_key of the source it was compiled from
+  uint64_t bytes;  // code object length
+  uint64_t sum;    // fnv1a of the code object
+};
+constexpr char kCacheMagic[8] = "VDSECJ1";
+
+bool cache_read(const std::string &path, uint64_t key, std::vector<char> &code) {
+  const std::string f = read_file(path);
+  if (f.empty()) return false;
+  CacheHeader h{};
+  bool ok = f.size() > sizeof h;
+  if (ok) {
+    std::memcpy(&h, f.data(), sizeof h);
+    ok = !std::memcmp(h.magic, kCacheMagic, sizeof h.magic) && h.key == key && h.bytes == f.size() - sizeof h &&
+         h.sum == fnv1a(f.data() + sizeof h, h.bytes);
+  }
+  if (!ok) {
+    (void)std::remove(path.c_str());
+    return false;
+  }
+  code.assign(f.begin() + sizeof h, f.end());
+  return true;
+}
+
+// Written to a unique temporary name in the cache directory (mkstemp), then
+// renamed: concurrent writers of one key never share a file, and readers see
+// a whole file or none.
+void cache_write(const std::string &path, uint64_t key, const std::vector<char> &code) {
+  std::string tmp = path + ".XXXXXX";
+  const int fd = mkstemp(&tmp[0]);
+  if (fd < 0) return;
+  CacheHeader h{};
+  std::memcpy(h.magic, kCacheMagic, sizeof h.magic);
+  h.key = key;
+  h.bytes = code.size();
+  h.sum = fnv1a(code.data(), code.size());
+  bool ok = write(fd, &h, sizeof h) == (ssize_t)sizeof h;
+  for (size_t at = 0; ok && at < code.size();) {
+    const ssize_t w = write(fd, code.data() + at, code.size() - at);
+    ok = w > 0;
+    if (ok) at += (size_t)w;
+  }
+  ok = (close(fd) == 0) && ok;
+  if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) (void)std::remove(tmp.c_str());
 }
 
 // Compile one survivor set's kernel with the helper (host only: no device
 // needed): source and code object pass through a private temporary directory.
-bool compile(const Key &key, std::vector<char> &code, std::string &log) {
+bool compile(const Key &key, std::vector<char> &code, std::string &log, std::string *cache_file = nullptr) {
   const std::string src = kernel_source(key);
   const std::string helper = helper_path();
   if (helper.empty() || access(helper.c_str(), X_OK) != 0) {
     log = "vds_ec_jitc not found next to libvds_ec.so";
     return false;
   }
-  const std::string cached = cache_path(src, helper);
-  if (!cached.empty()) {
-    const std::string bytes = read_file(cached);
-    if (!bytes.empty()) {
-      code.assign(bytes.begin(), bytes.end());
-      return true;
-    }
-  }
+  const uint64_t ckey = cache_key(src, helper);
+  const std::string cached = cache_path(ckey);
+  if (cache_file) *cache_file = cached;
+  if (!cached.empty() && cache_read(cached, ckey, code)) return true;
   const char *tmpenv = std::getenv("TMPDIR");
   std::string dir = std::string(tmpenv && *tmpenv ? tmpenv : "/tmp") + "/vds_ec_jit_XXXXXX";
   if (!mkdtemp(&dir[0])) {
@@ -307,24 +353,17 @@ bool compile(const Key &key, std::vector<char> &code, std::string &log) {
   std::remove(out.c_str());
   std::remove(err.c_str());
   rmdir(dir.c_str());
-  if (ok && !cached.empty()) {  // (best effort)
-    const std::string tmp = cached + "." + std::to_string((long)getpid()) + ".tmp";
-    if (FILE *f = std::fopen(tmp.c_str(), "wb")) {
-      const bool w = std::fwrite(code.data(), 1, code.size(), f) == code.size();
-      if (std::fclose(f) == 0 && w)
-        (void)std::rename(tmp.c_str(), cached.c_str());
-      else
-        std::remove(tmp.c_str());
-    }
-  }
+  if (ok && !cached.empty()) cache_write(cached, ckey, code);  // (best effort)
   return ok;
 }
 
 class Jit {
  public:
+  // Never destroyed (as HostPool): threads may still be inside function() at
+  // exit, and the worker may be waiting on a helper compile; it is detached.
   static Jit &get() {
-    static Jit j;
-    return j;
+    static Jit *j = new Jit();
+    return *j;
   }
 
   // The loaded kernel of `key` on the current device, or nullptr (not
@@ -360,22 +399,26 @@ class Jit {
         e = it->second;
       }
       if (e->state != Entry::kReady) return nullptr;
-      if (e->fn[dev]) return e->fn[dev];
+      if (hipFunction_t f = e->fn[dev].load(std::memory_order_acquire)) return f;
     }
     // first use on this device: load the code object (once per device)
     std::lock_guard<std::mutex> g(load_mu_);
-    if (!e->fn[dev]) {
-      hipModule_t m = nullptr;
-      hipFunction_t f = nullptr;
-      if (hipModuleLoadData(&m, e->code.data()) != hipSuccess) return nullptr;
-      if (hipModuleGetFunction(&f, m, "vds_ec_jit_restore") != hipSuccess) {
-        (void)hipModuleUnload(m);
-        return nullptr;
-      }
-      e->mod[dev] = m;
-      e->fn[dev] = f;
+    if (hipFunction_t f = e->fn[dev].load(std::memory_order_acquire)) return f;
+    hipModule_t m = nullptr;
+    hipFunction_t f = nullptr;
+    if (hipModuleLoadData(&m, e->code.data()) != hipSuccess ||
+        hipModuleGetFunction(&f, m, "vds_ec_jit_restore") != hipSuccess) {
+      if (m) (void)hipModuleUnload(m);
+      // remembered (the syndrome kernel serves the set from now on), and the
+      // cached file that gave it is dropped so the next process recompiles
+      std::lock_guard<std::mutex> lk(mu_);
+      e->state = Entry::kFailed;
+      if (!e->cache_file.empty()) (void)std::remove(e->cache_file.c_str());
+      return nullptr;
     }
-    return e->fn[dev];
+    e->mod[dev] = m;
+    e->fn[dev].store(f, std::memory_order_release);
+    return f;
   }
 
   bool ready(const Key &key) {
@@ -400,34 +443,24 @@ class Jit {
     return ok;
   }
 
-  ~Jit() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-      queue_.clear();
-    }
-    cv_.notify_all();
-    if (worker_.joinable()) worker_.join();
-  }
-
  private:
   void run(const Key &key, const std::shared_ptr<Entry> &e) {
     std::vector<char> code;
-    std::string log;
-    const bool ok = compile(key, code, log);
+    std::string log, file;
+    const bool ok = compile(key, code, log, &file);
     std::lock_guard<std::mutex> lk(mu_);
     e->code.swap(code);
     e->log.swap(log);
+    e->cache_file.swap(file);
     e->state = ok ? Entry::kReady : Entry::kFailed;
   }
 
   void start_worker() {  // (mu_ held)
-    if (worker_.joinable()) return;
+    if (worker_started_) return;
     worker_ = std::thread([this] {
       std::unique_lock<std::mutex> lk(mu_);
       while (true) {
-        cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
-        if (stop_) break;
+        cv_.wait(lk, [&] { return !queue_.empty(); });
         const Key key = queue_.front();
         queue_.pop_front();
         std::shared_ptr<Entry> e = map_[key];
@@ -438,8 +471,9 @@ class Jit {
         --busy_;
         if (queue_.empty() && busy_ == 0) idle_cv_.notify_all();
       }
-      idle_cv_.notify_all();
     });
+    worker_.detach();
+    worker_started_ = true;
   }
 
   std::mutex mu_, load_mu_;
@@ -448,8 +482,8 @@ class Jit {
   std::map<Key, int> seen_;
   std::deque<Key> queue_;
   std::thread worker_;
+  bool worker_started_ = false;
   int busy_ = 0;
-  bool stop_ = false;
 };
 
 Key key_of(uint32_t k, uint32_t n, const uint8_t *points, bool regen) {

@@ -11,7 +11,9 @@
 //   vds_ec_jitc SOURCE.hip OUT.co     exit 0: OUT.co written; else the log on stderr
 //
 // The kernel source includes the device headers embedded here at build time
-// (jit_embed.inc, vds_amd/build.py), the same set the library was built from.
+// (jit_embed.inc, vds_amd/build.py), the same set the library was built from,
+// and compiles for the architecture the library was built for (VDS_EC_ARCH_STR,
+// passed by build.py to both).
 #include <hip/hiprtc.h>
 
 #include <cstdio>
@@ -19,6 +21,10 @@
 #include <sstream>
 #include <string>
 #include <vector>
+
+#ifndef VDS_EC_ARCH_STR
+#define VDS_EC_ARCH_STR "gfx950"
+#endif
 
 namespace {
 struct EmbeddedFile {
@@ -52,7 +58,7 @@ int main(int argc, char **argv) {
     std::fprintf(stderr, "vds_ec_jitc: hiprtcCreateProgram failed\n");
     return 1;
   }
-  const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++20"};
+  const char *opts[] = {"--offload-arch=" VDS_EC_ARCH_STR, "-O3", "-std=c++20"};
   const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
   size_t ls = 0;
   hiprtcGetProgramLogSize(prog, &ls);

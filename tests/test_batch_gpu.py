@@ -34,7 +34,7 @@ def _first_k_found(rng, k, n_total, lost):
     return [r for r in range(n_total) if r not in gone][:k]
 
 
-@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 40), (32, 40), (32, 64)])
+@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 40), (32, 40), (32, 64), (16, 18), (32, 34)])
 def test_restore_batch_per_object_survivors(gpu, k, n_total):
     import torch
     from vds_amd import chunk
@@ -64,7 +64,7 @@ def test_restore_batch_per_object_survivors(gpu, k, n_total):
         assert (got[size:] == 0xA5).all(), size  # nothing written past the object
 
 
-@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 40), (32, 40), (32, 64)])
+@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 40), (32, 40), (32, 64), (16, 18), (32, 34)])
 def test_regenerate_batch_per_object(gpu, k, n_total):
     import torch
     from vds_amd import chunk

@@ -106,10 +106,11 @@ def test_restore_noncodeword_paths(gpu, k, nodes, T, path, pmode):
         assert (got[o, E:] == 0xA5).all(), "wrote past E"
 
 
-@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 48), (32, 40), (32, 64)])
+@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 48), (32, 40), (32, 64), (16, 17), (16, 18), (32, 33), (32, 34)])
 def test_restore_batch_noncodeword(gpu, k, n_total):
-    """Batch mode (k_restore_syn BATCH for survivors within its points, the
-    per-object fallback for the rest) on random survivors and trailers."""
+    """Batch mode (k_restore_syn BATCH for survivors within its points -- the
+    SMALL ms = 1, 2 kernels for survivors within 0..k, 0..k+1 -- the RT mode
+    and the per-object fallback for the rest) on random survivors and trailers."""
     import torch
     from vds_amd import chunk
     rng = np.random.default_rng(77 + k + n_total)
@@ -184,7 +185,7 @@ def test_regenerate_noncodeword_paths(gpu, k, nodes, targets, T, path, pmode):
             assert (got[i, o, L:] == 0x5A).all()
 
 
-@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 48), (32, 40), (32, 64)])
+@pytest.mark.parametrize("k,n_total", [(16, 20), (16, 48), (32, 40), (32, 64), (16, 18), (32, 34)])
 def test_regenerate_batch_noncodeword(gpu, k, n_total):
     """Batch regenerate (syndrome batch kernel + its device-side tail, and the
     per-object fallback) on random survivors with disagreeing trailers."""

@@ -19,6 +19,8 @@
 // the live temps of one block fit the register file.
 //
 //   gen_restore K N WAVES syndrome_block interp_block [half_block [half_split]] > restore_K_N_wW.inc
+//   gen_restore small K MS block > smallsyn_K_MS.inc   (see main_small)
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -214,8 +216,73 @@ static int main_fill(int argc, char **argv) {
   return 0;
 }
 
+// Small-M syndromes (k_restore_syn's SMALL batch mode, restore_syn.hpp): the
+// MS checks of the code restricted to the FIXED point set A = {0..K+MS-1},
+//   S_j = sum_{a in A} v_a a^j y_a,  v_a = 1 / prod_{b in A, b != a} (a + b),
+// which vanish on every codeword; with at most MS points of A erased (zeroed)
+// they determine the erased values through the MS x MS solve W_E^{-1}
+// (host).  The download loop's survivor sets are mostly of this shape: the
+// first k replicas found, with none or one or two of 0..k-1 lost.  Wave w
+// takes points 4w..4w+3 and, for w < MS, point K + w, and computes its share
+// of every S_j (one Paar program per wave); the shares meet in the syndrome
+// slots K + MS + j through LDS XOR atomics.
+static int main_small(int argc, char **argv) {
+  if (argc != 5) return 2;
+  const int K = std::atoi(argv[2]), MS = std::atoi(argv[3]), pb = std::atoi(argv[4]);
+  const int N = K + MS, WV = K / 4;
+  if (K % 4 || MS < 1 || MS > WV || 2 * MS > K / 4 || pb < 1) return 2;
+  std::vector<uint32_t> W((size_t)MS * N);
+  for (int a = 0; a < N; ++a) {
+    uint32_t prod = 1;
+    for (int b = 0; b < N; ++b)
+      if (b != a) prod = gf16_mul(prod, (uint32_t)(a ^ b));
+    const uint32_t v = gf16_inv(prod);
+    for (int j = 0; j < MS; ++j) W[(size_t)j * N + a] = gf16_mul(v, gf16_vandermonde(a, j));
+  }
+  std::printf("// GENERATED by tools/xorgen/gen_restore small %d %d %d -- do not edit.\n", K, MS, pb);
+  std::printf("// Small-M syndromes over the points 0..%d for k_restore_syn's SMALL batch mode (%d waves).\n", N - 1, WV);
+  std::printf("template <> struct SmallSyn<%d, %d> {\n", K, MS);
+  std::printf("  static constexpr bool kSmall = true;\n  static constexpr int kFill = -1;\n");
+  std::printf("  static constexpr bool kScatter = false;\n");
+  std::printf("  static constexpr int kM = %d, kN = %d, kSynSlot = %d;  // syndrome j in LDS slot kSynSlot + j\n", MS, N, N);
+  std::printf("  static constexpr uint16_t kW[%d][%d] = {\n", MS, N);
+  for (int j = 0; j < MS; ++j) {
+    std::printf("    {");
+    for (int a = 0; a < N; ++a) std::printf("0x%04x%s", W[(size_t)j * N + a], a + 1 < N ? ", " : "");
+    std::printf("},\n");
+  }
+  std::printf("  };\n");
+  size_t total = 0;
+  for (int w = 0; w < WV; ++w) {
+    std::vector<int> pts = {4 * w, 4 * w + 1, 4 * w + 2, 4 * w + 3};
+    if (w < MS) pts.push_back(K + w);
+    std::vector<uint32_t> Ww((size_t)MS * pts.size());
+    for (int j = 0; j < MS; ++j)
+      for (size_t i = 0; i < pts.size(); ++i) Ww[(size_t)j * pts.size() + i] = W[(size_t)j * N + pts[i]];
+    const auto rows = all_bitrows(Ww, MS, (int)pts.size());
+    xorgen::InputMap im;
+    im.map = pts;
+    char name[32];
+    std::snprintf(name, sizeof name, "part%d", w);
+    std::string s;
+    const size_t ops = xorgen::emit_program(s, name, rows, (int)pts.size(), row_range(0, 16 * MS), pb, im);
+    std::fputs(s.c_str(), stdout);
+    std::fprintf(stderr, "  %s: %zu ops\n", name, ops);
+    total += ops;
+  }
+  std::printf("  template <typename In>\n  __device__ __forceinline__ static void part(int w, const In &IN4, uint32_t (&acc)[%d]) {\n",
+              16 * MS);
+  std::printf("    switch (w) {\n");
+  for (int w = 0; w < WV; ++w) std::printf("      case %d: part%d(IN4, acc); break;\n", w, w);
+  std::printf("      default: break;\n    }\n  }\n");
+  std::printf("  static constexpr int kXorOps = %zu;\n};\n", total);
+  std::fprintf(stderr, "small K=%d MS=%d: %zu XOR instructions per 32 stripes\n", K, MS, total);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   if (argc > 1 && std::string(argv[1]) == "fill") return main_fill(argc, argv);
+  if (argc > 1 && std::string(argv[1]) == "small") return main_small(argc, argv);
   if (argc < 6 || argc > 8) {
     std::fprintf(stderr, "usage: %s K N WAVES syndrome_block interp_block [half_interp_block [half_split]]\n", argv[0]);
     return 2;

@@ -178,10 +178,22 @@ struct SynBatchObj {
   uint32_t first;                    // plan position (RT: slot) of the caller's chunk 0 (whose trailer restore reads)
   SynBatchRt rt;                     // RT mode only
 };
+// SMALL batch mode (small-M syndromes, restore_syn.hpp): the survivors lie in
+// A = {0..K+MS-1} (MS <= kSmallMaxM), so the MS checks over A and an MS x MS
+// solve give the erased points; the rows recovered are erased[0..nrec).
+constexpr int kSmallMaxM = 2;
 struct SynBatchPlan {
-  uint8_t erased[kMaxFastK / 4];
-  uint8_t point[kMaxFastK];               // the survivors' points, ascending
-  uint32_t solve_sel[kMaxFastK / 4][4];  // as SynRestoreArgs::solve_sel
+  uint8_t erased[kMaxFastK / 4];  // SMALL: A's MS erased points ascending, then the syndrome slots
+  uint8_t point[kMaxFastK];       // the survivors' points, ascending
+  union {
+    uint32_t solve_sel[kMaxFastK / 4][4];  // as SynRestoreArgs::solve_sel
+    // SMALL: bit b of small_mask[m][j][i] = bit i of R[m][j] x^b (R = W_E^{-1}):
+    // output plane i of recovered row m is the XOR over j, b of syndrome j's
+    // plane b where the bit is set
+    uint16_t small_mask[kSmallMaxM][kSmallMaxM][16];
+  };
+  uint32_t nrec;  // SMALL: rows recovered (restore: erased points below K; regenerate: MS; 0 = none)
+  uint32_t pad_;
 };
 struct SynBatchTile {
   uint32_t obj[2];      // object of each half (an unused half: the batch's empty object)
@@ -254,6 +266,12 @@ bool jit_enabled();  // mode != 0 (vds_ec_jit_set_mode)
 hipError_t launch_restore_syn_jit(hipFunction_t fn, uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s);
 // a.objs / a.plans / a.tiles / a.total_tiles set; the other fields unused
 hipError_t launch_restore_syn_batch(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen);
+// SMALL batch mode over the points 0..k+ms-1 (ms = 1, 2; k = 16, 32): tables as
+// launch_restore_syn_batch, plans with small_mask / nrec.
+bool has_restore_small(uint32_t k, uint32_t ms);
+// W[j][a] = v_a a^j of the ms checks over A = {0..k+ms-1}; nullptr if not compiled.
+const uint16_t *restore_small_weights(uint32_t k, uint32_t ms);
+hipError_t launch_restore_small_batch(uint32_t k, uint32_t ms, const SynRestoreArgs &a, hipStream_t s, bool regen);
 hipError_t launch_regen_generic(const RegenArgs &a, hipStream_t s);
 hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s);
 // Returns hipErrorNotSupported when no bit-sliced instantiation exists for (k, n).

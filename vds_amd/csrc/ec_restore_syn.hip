@@ -21,6 +21,10 @@ namespace vds_ec {
 #define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #include "generated/restore_16_20_w4.inc"
 #include "generated/restore_32_40_w8.inc"
+#include "generated/smallsyn_16_1.inc"
+#include "generated/smallsyn_16_2.inc"
+#include "generated/smallsyn_32_1.inc"
+#include "generated/smallsyn_32_2.inc"
 #undef VDS_SCHED_FENCE
 
 template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false, class FillP = NoFill>
@@ -108,6 +112,31 @@ hipError_t launch_restore_syn_batch(uint32_t k, uint32_t n, const SynRestoreArgs
     return regen ? launch_restore_syn_kn<16, 20, 4, true, true>(a, s) : launch_restore_syn_kn<16, 20, 4, false, true>(a, s);
   if (k == 32 && n == 40)
     return regen ? launch_restore_syn_kn<32, 40, 8, true, true>(a, s) : launch_restore_syn_kn<32, 40, 8, false, true>(a, s);
+  return hipErrorNotSupported;
+}
+
+bool has_restore_small(uint32_t k, uint32_t ms) { return (k == 16 || k == 32) && (ms == 1 || ms == 2); }
+
+const uint16_t *restore_small_weights(uint32_t k, uint32_t ms) {
+  if (k == 16 && ms == 1) return &SmallSyn<16, 1>::kW[0][0];
+  if (k == 16 && ms == 2) return &SmallSyn<16, 2>::kW[0][0];
+  if (k == 32 && ms == 1) return &SmallSyn<32, 1>::kW[0][0];
+  if (k == 32 && ms == 2) return &SmallSyn<32, 2>::kW[0][0];
+  return nullptr;
+}
+
+template <int K, int N, int WV, int MS>
+static hipError_t launch_small_kn(const SynRestoreArgs &a, hipStream_t s, bool regen) {
+  static_assert(SmallSyn<K, MS>::kSynSlot + MS <= N, "syndrome slots inside the LDS points");
+  return regen ? launch_restore_syn_kn<K, N, WV, true, true, false, SmallSyn<K, MS>>(a, s)
+               : launch_restore_syn_kn<K, N, WV, false, true, false, SmallSyn<K, MS>>(a, s);
+}
+
+hipError_t launch_restore_small_batch(uint32_t k, uint32_t ms, const SynRestoreArgs &a, hipStream_t s, bool regen) {
+  if (k == 16 && ms == 1) return launch_small_kn<16, 20, 4, 1>(a, s, regen);
+  if (k == 16 && ms == 2) return launch_small_kn<16, 20, 4, 2>(a, s, regen);
+  if (k == 32 && ms == 1) return launch_small_kn<32, 40, 8, 1>(a, s, regen);
+  if (k == 32 && ms == 2) return launch_small_kn<32, 40, 8, 2>(a, s, regen);
   return hipErrorNotSupported;
 }
 

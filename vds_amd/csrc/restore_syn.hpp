@@ -463,11 +463,26 @@ __device__ __forceinline__ void st16_guard(uint8_t *p, u32x4 v, int64_t valid) {
 struct NoFill {
   static constexpr int kFill = -1;
   static constexpr bool kScatter = false;
+  static constexpr bool kSmall = false;
 };
+// SMALL (batch only): FillP = SmallSyn<K, MS> (generated/smallsyn_K_MS.inc).
+// The survivors lie in A = {0..K+MS-1}: the MS checks of the code restricted
+// to A, S_j = sum_{a in A} v_a a^j y_a (erased points zero), determine A's
+// erased points through the plan's MS x MS solve.  Wave w computes its share
+// of every S_j from its fixed points (4w..4w+3, and K + w for w < MS) and adds
+// it into the syndrome slots with LDS XOR atomics; after a barrier, wave w
+// forms planes (16/WV) w.. of every recovered point with the plan's bit masks
+// and writes them into the point's zeroed slot.  A plan with nothing to
+// recover (restore: no erased point below K) skips the phase, barriers and
+// all.  Against the N = K + K/4 syndrome kernel at MS = 2: 2.4K instead of
+// 13.4K syndrome XORs per tile (k = 32), and no M x M runtime walk.
+template <int K, int MS> struct SmallSyn;
 template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false, class FillP = NoFill>
 __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   constexpr bool FILL = FillP::kFill >= 0;
   constexpr bool kScatter = FILL && FillP::kScatter;
+  constexpr bool kSmall = FillP::kSmall;
+  static_assert(!kSmall || (BATCH && !RT && !FILL), "SMALL is a batch mode of its own");
   using S = SynShape<K, N, WV>;
   using P = typename S::P;
   constexpr bool kPrio = S::kPrio;
@@ -735,6 +750,54 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       // (its own stage-1 slots in, LDS XOR atomics out; survivors sorted by point)
       syn_scatter_fill<WV, FillP, 0>(wave, L);
       if (!kLateLoad) prefetch(tile + t_step);
+    } else if constexpr (kSmall) {
+      // ---- 2 (SMALL). the MS checks over A, then the MS x MS recovery
+      const uint32_t nrec = s_ld(&pl->nrec);
+      if (nrec != 0) {
+        {
+          uint32_t acc[16 * FillP::kM];
+          FillP::part(wave, L, acc);
+#pragma unroll
+          for (int j = 0; j < FillP::kM; ++j)
+            lds_xor_point(L, FillP::kSynSlot + j, *reinterpret_cast<const Plane16 *>(acc + 16 * j));
+        }
+        st.mark(2);
+        __syncthreads();  // the syndromes are whole
+        st.mark(3);
+        constexpr int PW = 16 / WV;  // planes of each recovered point formed by this wave
+        static_assert(PW == 2 || PW == 4, "plane split: 8 or 4 waves");
+        uint32_t sy[FillP::kM][16];
+#pragma unroll
+        for (int j = 0; j < FillP::kM; ++j) syn_get_point(L, FillP::kSynSlot + j, sy[j]);
+#pragma unroll
+        for (int m = 0; m < FillP::kM; ++m) {
+          if ((uint32_t)m >= nrec) break;
+          uint32_t o[PW];
+#pragma unroll
+          for (int i = 0; i < PW; ++i) o[i] = 0u;
+#pragma unroll
+          for (int j = 0; j < FillP::kM; ++j) {
+            // this wave's PW masks of R[m][j] (16 bits each, one scalar load)
+            uint64_t mk;
+            if constexpr (PW == 2)
+              mk = s_ld(reinterpret_cast<const uint32_t *>(&pl->small_mask[m][j][PW * wave]));
+            else
+              mk = s_ld(reinterpret_cast<const uint64_t *>(&pl->small_mask[m][j][PW * wave]));
+#pragma unroll
+            for (int i = 0; i < PW; ++i)
+#pragma unroll
+              for (int b = 0; b < 16; ++b) o[i] ^= sy[j][b] & (0u - (uint32_t)((mk >> (16 * i + b)) & 1u));
+          }
+          // planes PW w .. PW w + PW - 1 of point erased[m]: 4 PW bytes of
+          // this lane's 16-byte word of group (PW w) / 4
+          const int e = (int)s_ld_u8(pl->erased, m);
+          lds_char *dst = L.at(4 * e + (PW * wave) / 4) + 4 * ((PW * wave) % 4);
+          if constexpr (PW == 2)
+            *(__attribute__((address_space(3))) u32x2 *)dst = u32x2{o[0], o[1]};
+          else
+            *(lds_v4 *)dst = u32x4{o[0], o[1], o[2], o[3]};
+        }
+      }
     } else if constexpr (FILL) {
       if (wave < FillP::kFill) {
         uint32_t acc[16];

@@ -1247,10 +1247,65 @@ SynPlanStore &syn_plan_store() {
   return *st;
 }
 
-// The plan of the erased set ~seen (k, n = k + k/4 compiled): points and
-// erased points ascending, the solve from the store or computed.
-bool syn_plan(uint32_t k, uint32_t n, uint64_t seen, SynBatchPlan *out) {
-  const uint64_t key = (~seen & ((1ull << n) - 1)) | ((uint64_t)k << 56);
+// The SMALL plan of survivor set `seen` within A = {0..k+ms-1}: A's ms erased
+// points ascending (then the syndrome slots, which stage 1 zeroes too), the
+// survivors ascending, R = W_E^{-1} of the ms checks over A as bit masks, and
+// nrec = the erased points below k (the rows a restore needs).
+bool small_plan_solve(uint32_t k, uint32_t ms, uint64_t seen, SynBatchPlan &p) {
+  const uint16_t *W = restore_small_weights(k, ms);
+  const uint32_t na = k + ms;
+  if (!W || ms > (uint32_t)kSmallMaxM) return false;
+  uint32_t e = 0, j = 0, nrec = 0;
+  for (uint32_t a = 0; a < na; ++a) {
+    if ((seen >> a) & 1u) {
+      p.point[j++] = (uint8_t)a;
+    } else {
+      p.erased[e++] = (uint8_t)a;
+      nrec += a < k;
+    }
+  }
+  if (j != k || e != ms) return false;
+  for (uint32_t i = ms; i < kMaxFastK / 4; ++i) p.erased[i] = (uint8_t)(na + std::min(i - ms, ms - 1));
+  // [W_E | I] -> [I | R] (ms <= 2; W_E[j][i] = v_e e^j at erased point i)
+  uint32_t A[kSmallMaxM][2 * kSmallMaxM] = {};
+  for (uint32_t r = 0; r < ms; ++r) {
+    for (uint32_t i = 0; i < ms; ++i) A[r][i] = W[r * na + p.erased[i]];
+    A[r][ms + r] = 1;
+  }
+  for (uint32_t c = 0; c < ms; ++c) {
+    uint32_t piv = c;
+    while (piv < ms && A[piv][c] == 0) ++piv;
+    if (piv == ms) return false;
+    if (piv != c)
+      for (uint32_t x = 0; x < 2 * ms; ++x) std::swap(A[c][x], A[piv][x]);
+    const uint32_t iv = gf16_inv_fast(A[c][c]);
+    for (uint32_t x = 0; x < 2 * ms; ++x) A[c][x] = gf16_mul_fast(A[c][x], iv);
+    for (uint32_t r = 0; r < ms; ++r) {
+      const uint32_t f = A[r][c];
+      if (r == c || f == 0) continue;
+      for (uint32_t x = 0; x < 2 * ms; ++x) A[r][x] ^= gf16_mul_fast(f, A[c][x]);
+    }
+  }
+  std::memset(p.small_mask, 0, sizeof p.small_mask);
+  for (uint32_t m = 0; m < ms; ++m)
+    for (uint32_t jj = 0; jj < ms; ++jj) {
+      const uint32_t r = A[m][ms + jj];
+      for (uint32_t b = 0; b < 16; ++b) {
+        const uint32_t v = gf16_mul_fast(r, 1u << b);
+        for (uint32_t i = 0; i < 16; ++i)
+          if ((v >> i) & 1u) p.small_mask[m][jj][i] |= (uint16_t)(1u << b);
+      }
+    }
+  p.nrec = nrec;
+  return true;
+}
+
+// The plan of the erased set ~seen (k, n = k + k/4 compiled; or, ms > 0, the
+// SMALL plan over 0..k+ms-1): points and erased points ascending, the solve
+// from the store or computed.
+bool syn_plan(uint32_t k, uint32_t n, uint64_t seen, SynBatchPlan *out, uint32_t ms = 0) {
+  if (ms) n = k + ms;
+  const uint64_t key = (~seen & ((1ull << n) - 1)) | ((uint64_t)k << 56) | ((uint64_t)ms << 48);
   SynPlanStore &st = syn_plan_store();
   {
     std::lock_guard<std::mutex> g(st.mu);
@@ -1260,19 +1315,23 @@ bool syn_plan(uint32_t k, uint32_t n, uint64_t seen, SynBatchPlan *out) {
       return true;
     }
   }
-  SynRestoreArgs sa{};
-  uint32_t e = 0, j = 0;
-  for (uint32_t a = 0; a < n; ++a) {
-    if ((seen >> a) & 1u)
-      sa.point[j++] = (uint8_t)a;
-    else
-      sa.erased[e++] = (uint8_t)a;
-  }
-  if (j != k || !syn_solve(k, n, sa)) return false;
   SynBatchPlan p{};
-  std::memcpy(p.erased, sa.erased, sizeof p.erased);
-  std::memcpy(p.point, sa.point, sizeof p.point);
-  std::memcpy(p.solve_sel, sa.solve_sel, sizeof p.solve_sel);
+  if (ms) {
+    if (!small_plan_solve(k, ms, seen, p)) return false;
+  } else {
+    SynRestoreArgs sa{};
+    uint32_t e = 0, j = 0;
+    for (uint32_t a = 0; a < n; ++a) {
+      if ((seen >> a) & 1u)
+        sa.point[j++] = (uint8_t)a;
+      else
+        sa.erased[e++] = (uint8_t)a;
+    }
+    if (j != k || !syn_solve(k, n, sa)) return false;
+    std::memcpy(p.erased, sa.erased, sizeof p.erased);
+    std::memcpy(p.point, sa.point, sizeof p.point);
+    std::memcpy(p.solve_sel, sa.solve_sel, sizeof p.solve_sel);
+  }
   std::lock_guard<std::mutex> g(st.mu);
   if (st.map.size() >= SynPlanStore::kMax) st.map.clear();
   st.map.emplace(key, p);
@@ -1395,7 +1454,25 @@ struct BatchObjInfo {
   uint16_t rows;    // RT rows: restore, its erased points below k; regenerate, its targets
   uint8_t route;
   uint8_t parts;    // RT descriptors (regenerate: rows in groups of at most n - k)
+  uint8_t ms;       // kRouteSyn: SMALL ms (1, 2) over 0..k+ms-1, or 0 = the N = k + k/4 kernel
 };
+
+// The SMALL batch kernels (VDS_EC_SMALL=0 routes their objects to the
+// N = k + k/4 syndrome kernel instead: A/B).
+bool small_enabled() {
+  static const bool on = [] {
+    const char *v = std::getenv("VDS_EC_SMALL");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+// The smallest SMALL ms whose points 0..k+ms-1 hold every survivor (maxid), or 0.
+uint8_t small_ms_for(uint32_t k, uint32_t maxid) {
+  if (!small_enabled()) return 0;
+  for (uint32_t ms = 1; ms <= (uint32_t)kSmallMaxM; ++ms)
+    if (maxid < k + ms && has_restore_small(k, ms)) return (uint8_t)ms;
+  return 0;
+}
 
 // The survivor ids of one object: those below 64 as bits, the largest; false
 // when two coincide (V_S singular).
@@ -1424,6 +1501,11 @@ inline bool id_set(uint32_t k, const uint16_t *nd, uint64_t *seen, uint32_t *max
 // descriptor i and may run on several threads for distinct i.
 struct SynBatchBuild {
   uint32_t k, n;
+  bool regen = false;
+  // plans [0, cls_end[0]) are SMALL ms = 1, [cls_end[0], cls_end[1]) ms = 2,
+  // the rest the N = k + k/4 syndrome kernel's (batch_begin resolves them in
+  // that order); each class is one launch over its plans' tiles
+  uint32_t cls_end[2] = {0, 0};
   ParamSlot *slot = nullptr;
   size_t cap_objs = 0, cap_tiles = 0, cap_plans = 0, o_tiles = 0, o_plans = 0;
   SynBatchObj *objs = nullptr;
@@ -1460,14 +1542,17 @@ struct SynBatchBuild {
     hval.assign(1ull << bits, 0);
     hshift = 64 - bits;
   }
-  // The plan of survivor set `seen` (UINT32_MAX: no solve; not for distinct points).
-  uint32_t plan_of(uint64_t seen) {
+  // The plan of survivor set `seen` (UINT32_MAX: no solve; not for distinct
+  // points); ms > 0: the SMALL plan over 0..k+ms-1 (a set always resolves to
+  // the same ms within a call: the route is a function of the set).
+  uint32_t plan_of(uint64_t seen, uint32_t ms = 0) {
     const size_t mask = hkey.size() - 1;
     size_t i = (size_t)((seen * 0x9E3779B97F4A7C15ull) >> hshift);
     while (hkey[i] != 0 && hkey[i] != seen) i = (i + 1) & mask;
     if (hkey[i] == seen) return hval[i];
     SynBatchPlan pl;
-    if (!syn_plan(k, n, seen, &pl)) return UINT32_MAX;
+    if (!syn_plan(k, n, seen, &pl, ms)) return UINT32_MAX;
+    if (ms && regen) pl.nrec = ms;  // (regenerate: every erased point of A is a target candidate)
     const uint32_t p = (uint32_t)plans.size();
     plans.push_back(pl);
     hkey[i] = seen;
@@ -1526,10 +1611,20 @@ struct SynBatchBuild {
     if (e == hipSuccess) {
       SynRestoreArgs sa{};
       sa.objs = reinterpret_cast<const SynBatchObj *>(slot->d);
-      sa.tiles = reinterpret_cast<const SynBatchTile *>(slot->d + o_tiles);
       sa.plans = reinterpret_cast<const SynBatchPlan *>(slot->d + o_plans);
-      sa.total_tiles = (uint32_t)ntiles;
-      e = launch_restore_syn_batch(k, n, sa, s, regen);
+      const SynBatchTile *dt = reinterpret_cast<const SynBatchTile *>(slot->d + o_tiles);
+      // one launch per class, over its plans' contiguous tile range
+      const uint32_t bound[3] = {cls_end[0], cls_end[1], (uint32_t)plans.size()};
+      uint32_t p0 = 0;
+      for (int c = 0; c < 3 && e == hipSuccess; ++c) {
+        const uint64_t t0 = first[p0], t1 = first[bound[c]];
+        p0 = bound[c];
+        if (t1 == t0) continue;
+        sa.tiles = dt + t0;
+        sa.total_tiles = (uint32_t)(t1 - t0);
+        e = c < 2 ? launch_restore_small_batch(k, (uint32_t)c + 1, sa, s, regen)
+                  : launch_restore_syn_batch(k, n, sa, s, regen);
+      }
       // (reads the same tables, so before the slot is released)
       if (e == hipSuccess && regen) e = launch_regen_tail_batch(k, n - k, sa.objs, sa.plans, nobj, s);
     }
@@ -1702,12 +1797,19 @@ int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, Syn
   if (ix.nrt) rb.attach(sl[nb++]);
   if (ix.nsyn) {
     plan.assign(info.size(), 0);
-    for (uint32_t o = 0; o < info.size(); ++o)
-      if (info[o].route == kRouteSyn && (plan[o] = bb.plan_of(info[o].seen)) == UINT32_MAX) {
-        bb.abandon(s);
-        if (ix.nrt) rb.abandon(s);
-        return VDS_EC_ESINGULAR;
-      }
+    // SMALL ms = 1 plans first, then ms = 2, then the N = k + k/4 kernel's
+    // (SynBatchBuild::cls_end)
+    const uint8_t order[3] = {1, 2, 0};
+    for (int c = 0; c < 3; ++c) {
+      for (uint32_t o = 0; o < info.size(); ++o)
+        if (info[o].route == kRouteSyn && info[o].ms == order[c] &&
+            (plan[o] = bb.plan_of(info[o].seen, info[o].ms)) == UINT32_MAX) {
+          bb.abandon(s);
+          if (ix.nrt) rb.abandon(s);
+          return VDS_EC_ESINGULAR;
+        }
+      if (c < 2) bb.cls_end[c] = (uint32_t)bb.plans.size();
+    }
   }
   return VDS_EC_OK;
 }
@@ -1757,6 +1859,7 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
         f.route = kRouteSkip;
       } else if (syn && fits && maxid < n) {
         f.route = kRouteSyn;
+        f.ms = small_ms_for(k, maxid);
       } else if (batch_ok && fits && maxid < 256) {
         f.route = kRouteRt;
         f.parts = 1;
@@ -1861,6 +1964,7 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
       }
       if (ok) {
         f.route = kRouteSyn;
+        f.ms = small_ms_for(k, std::max(maxid, tmax));  // (every target an erased point of 0..k+ms-1)
       } else if (batch_ok && fits && maxid < 256 && tmax < 256) {
         f.route = kRouteRt;
         f.parts = (uint8_t)((nt + R - 1) / R);
@@ -1879,6 +1983,7 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
   BatchIndex ix;
   ix.build(info);
   SynBatchBuild bb{k, n};
+  bb.regen = true;
   RtBatchBuild rb{k, n};
   std::vector<uint32_t> plan;
   if ((rc = batch_begin(info, ix, bb, rb, plan, s))) return rc;
@@ -1891,7 +1996,8 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
       uint8_t *const *os = outs + (uint64_t)o * nt;
       if (f.route == kRouteSyn) {
         SynBatchObj &d = bb.fill(ix.syn[o], f.seen, nd, ch, plan[o], f.halves);
-        const uint64_t erased = ~f.seen & ((1ull << n) - 1);
+        const uint32_t np = f.ms ? k + f.ms : n;  // the plan's points
+        const uint64_t erased = ~f.seen & ((1ull << np) - 1);
         std::memset(d.regen, 0, sizeof d.regen);
         for (uint32_t i = 0; i < nt; ++i)
           d.regen[__builtin_popcountll(erased & ((1ull << tg[i]) - 1))] = os[i];

@@ -270,3 +270,41 @@ def test_batch_rejects_duplicate_ids_before_enqueue(gpu):
     assert e.value.status == ESINGULAR
     torch.cuda.synchronize()
     assert (out.cpu().numpy() == 0xA5).all() and (rg.cpu().numpy() == 0x5A).all(), "partial output"
+
+
+@pytest.mark.parametrize("k", [16, 32])
+def test_regenerate_batch_perm_noncodeword(gpu, k):
+    """The PERM batch regenerate (survivors exactly 0..k-1 in any order, one
+    target t in k..2k-1: P(t) = sum_c l_c(k) y_(c ^ (t - k)), one fixed program
+    read through a permuted address): random survivors and trailers, every
+    target of k..2k-1, sizes across the half-tile boundaries, against the
+    oracle's restore -> re-encode route."""
+    import torch
+    from vds_amd import chunk
+    rng = np.random.default_rng(4100 + k)
+    Ts = [0, 1, 5, 1023, 1024, 1025, 2048, 3000]
+    pvals = [0, 1, 2 * k - 1, 2 * k - 2, 2 * k, 7]
+    nodes, chunks, csz, targets, outs, want, keep = [], [], [], [], [], [], []
+    for i in range(2 * k + 5):
+        T = Ts[i % len(Ts)]
+        p = pvals[i % len(pvals)]
+        if T == 0:
+            p = 0 if i % 2 else 2 * k
+        sv = _survivors(rng, k, T, p, vary=True)
+        nd = list(range(k)) if i % 3 else list(rng.permutation(k))
+        t = k + (i % k) if i < 2 * k else int(rng.integers(k, 2 * k))
+        bufs = [torch.from_numpy(b).cuda() for b in sv]
+        keep.append(bufs)
+        nodes.append(nd)
+        chunks.append([b.data_ptr() for b in bufs])
+        csz.append(2 * T + 2)
+        targets.append([t])
+        want.append(_ref_regen(k, nd, sv, [t]))
+        outs.append([torch.full((2 * T + 2 + 16,), 0x5A, dtype=torch.uint8, device="cuda")])
+    chunk.regenerate_batch_device(k, nodes, chunks, csz, targets, [[o.data_ptr() for o in os_] for os_ in outs])
+    torch.cuda.synchronize()
+    for i, (ws, os_) in enumerate(zip(want, outs)):
+        L = csz[i]
+        g = os_[0].cpu().numpy()
+        assert np.array_equal(g[:L], ws[0]), (i, L, targets[i])
+        assert (g[L:] == 0x5A).all()

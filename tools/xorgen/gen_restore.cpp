@@ -20,6 +20,7 @@
 //
 //   gen_restore K N WAVES syndrome_block interp_block [half_block [half_split]] > restore_K_N_wW.inc
 //   gen_restore small K MS block > smallsyn_K_MS.inc   (see main_small)
+//   gen_restore perm K block > permsyn_K.inc            (see main_perm)
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -242,7 +243,7 @@ static int main_small(int argc, char **argv) {
   std::printf("// GENERATED by tools/xorgen/gen_restore small %d %d %d -- do not edit.\n", K, MS, pb);
   std::printf("// Small-M syndromes over the points 0..%d for k_restore_syn's SMALL batch mode (%d waves).\n", N - 1, WV);
   std::printf("template <> struct SmallSyn<%d, %d> {\n", K, MS);
-  std::printf("  static constexpr bool kSmall = true;\n  static constexpr int kFill = -1;\n");
+  std::printf("  static constexpr bool kSmall = true, kPerm = false;\n  static constexpr int kFill = -1;\n");
   std::printf("  static constexpr bool kScatter = false;\n");
   std::printf("  static constexpr int kM = %d, kN = %d, kSynSlot = %d;  // syndrome j in LDS slot kSynSlot + j\n", MS, N, N);
   std::printf("  static constexpr uint16_t kW[%d][%d] = {\n", MS, N);
@@ -280,7 +281,60 @@ static int main_small(int argc, char **argv) {
   return 0;
 }
 
+// PERM (k_restore_syn's PERM batch regenerate, restore_syn.hpp): survivors
+// exactly U = {0..K-1} (K = 2^m: U is the GF(2)-span of 1, x, .., x^(m-1)),
+// one target t = K + t' with t' in U.  Q(X) = P(X + t') has the same degree
+// and Q(c) = P(c + t') for c in U, so
+//   P(t) = Q(K) = sum_{c in U} l_c(K) y_{c + t'},  l_c(K) = prod_{b != c} (K + b) / (c + b):
+// ONE fixed program for every target of K..2K-1, its inputs read through the
+// runtime address permutation c -> c XOR t'.  Wave w takes points 4w..4w+3.
+static int main_perm(int argc, char **argv) {
+  if (argc != 4) return 2;
+  const int K = std::atoi(argv[2]), pb = std::atoi(argv[3]), WV = K / 4;
+  if (K < 4 || (K & (K - 1)) || pb < 1) return 2;
+  std::vector<uint32_t> l(K);
+  for (int c = 0; c < K; ++c) {
+    uint32_t num = 1, den = 1;
+    for (int b = 0; b < K; ++b)
+      if (b != c) {
+        num = gf16_mul(num, (uint32_t)(K ^ b));
+        den = gf16_mul(den, (uint32_t)(c ^ b));
+      }
+    l[c] = gf16_mul(num, gf16_inv(den));
+  }
+  std::printf("// GENERATED by tools/xorgen/gen_restore perm %d %d -- do not edit.\n", K, pb);
+  std::printf("// P(K + t') = sum_c l_c(K) y_(c ^ t') for k_restore_syn's PERM batch regenerate (%d waves).\n", WV);
+  std::printf("template <> struct PermSyn<%d> {\n", K);
+  std::printf("  static constexpr bool kSmall = false, kPerm = true, kScatter = false;\n  static constexpr int kFill = -1;\n");
+  std::printf("  static constexpr uint16_t kL[%d] = {", K);
+  for (int c = 0; c < K; ++c) std::printf("0x%04x%s", l[c], c + 1 < K ? ", " : "");
+  std::printf("};\n");
+  size_t total = 0;
+  for (int w = 0; w < WV; ++w) {
+    std::vector<uint32_t> Ww(4);
+    for (int i = 0; i < 4; ++i) Ww[i] = l[4 * w + i];
+    const auto rows = all_bitrows(Ww, 1, 4);
+    xorgen::InputMap im;
+    im.map = {4 * w, 4 * w + 1, 4 * w + 2, 4 * w + 3};
+    char name[32];
+    std::snprintf(name, sizeof name, "part%d", w);
+    std::string s;
+    const size_t ops = xorgen::emit_program(s, name, rows, 4, row_range(0, 16), pb, im);
+    std::fputs(s.c_str(), stdout);
+    std::fprintf(stderr, "  %s: %zu ops\n", name, ops);
+    total += ops;
+  }
+  std::printf("  template <typename In>\n  __device__ __forceinline__ static void part(int w, const In &IN4, uint32_t (&acc)[16]) {\n");
+  std::printf("    switch (w) {\n");
+  for (int w = 0; w < WV; ++w) std::printf("      case %d: part%d(IN4, acc); break;\n", w, w);
+  std::printf("      default: break;\n    }\n  }\n");
+  std::printf("  static constexpr int kXorOps = %zu;\n};\n", total);
+  std::fprintf(stderr, "perm K=%d: %zu XOR instructions per 32 stripes\n", K, total);
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 1 && std::string(argv[1]) == "perm") return main_perm(argc, argv);
   if (argc > 1 && std::string(argv[1]) == "fill") return main_fill(argc, argv);
   if (argc > 1 && std::string(argv[1]) == "small") return main_small(argc, argv);
   if (argc < 6 || argc > 8) {

@@ -272,6 +272,9 @@ bool has_restore_small(uint32_t k, uint32_t ms);
 // W[j][a] = v_a a^j of the ms checks over A = {0..k+ms-1}; nullptr if not compiled.
 const uint16_t *restore_small_weights(uint32_t k, uint32_t ms);
 hipError_t launch_restore_small_batch(uint32_t k, uint32_t ms, const SynRestoreArgs &a, hipStream_t s, bool regen);
+// PERM batch regenerate (k = 16, 32): survivors exactly 0..k-1, one target
+// t = erased[0] of each plan in k..2k-1.
+hipError_t launch_regen_perm_batch(uint32_t k, const SynRestoreArgs &a, hipStream_t s);
 hipError_t launch_regen_generic(const RegenArgs &a, hipStream_t s);
 hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s);
 // Returns hipErrorNotSupported when no bit-sliced instantiation exists for (k, n).

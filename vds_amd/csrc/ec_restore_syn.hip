@@ -25,6 +25,8 @@ namespace vds_ec {
 #include "generated/smallsyn_16_2.inc"
 #include "generated/smallsyn_32_1.inc"
 #include "generated/smallsyn_32_2.inc"
+#include "generated/permsyn_16.inc"
+#include "generated/permsyn_32.inc"
 #undef VDS_SCHED_FENCE
 
 template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false, class FillP = NoFill>
@@ -137,6 +139,12 @@ hipError_t launch_restore_small_batch(uint32_t k, uint32_t ms, const SynRestoreA
   if (k == 16 && ms == 2) return launch_small_kn<16, 20, 4, 2>(a, s, regen);
   if (k == 32 && ms == 1) return launch_small_kn<32, 40, 8, 1>(a, s, regen);
   if (k == 32 && ms == 2) return launch_small_kn<32, 40, 8, 2>(a, s, regen);
+  return hipErrorNotSupported;
+}
+
+hipError_t launch_regen_perm_batch(uint32_t k, const SynRestoreArgs &a, hipStream_t s) {
+  if (k == 16) return launch_restore_syn_kn<16, 20, 4, true, true, false, PermSyn<16>>(a, s);
+  if (k == 32) return launch_restore_syn_kn<32, 40, 8, true, true, false, PermSyn<32>>(a, s);
   return hipErrorNotSupported;
 }
 

@@ -464,7 +464,15 @@ struct NoFill {
   static constexpr int kFill = -1;
   static constexpr bool kScatter = false;
   static constexpr bool kSmall = false;
+  static constexpr bool kPerm = false;
 };
+// PERM (batch regenerate only): FillP = PermSyn<K> (generated/permsyn_K.inc).
+// Survivors exactly U = {0..K-1}, one target t = K + t' (t' in U): P(t) =
+// sum_c l_c(K) y_(c ^ t') -- one fixed program for every such target, its
+// LDS reads permuted by the plan's t' (gen_restore.cpp main_perm).  Wave w
+// adds its four points' share into slot K; wave 0 stores it as replica t.
+// The plan's erased[0] is t (the regenerate tail reads it there too).
+template <int K> struct PermSyn;
 // SMALL (batch only): FillP = SmallSyn<K, MS> (generated/smallsyn_K_MS.inc).
 // The survivors lie in A = {0..K+MS-1}: the MS checks of the code restricted
 // to A, S_j = sum_{a in A} v_a a^j y_a (erased points zero), determine A's
@@ -482,7 +490,9 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   constexpr bool FILL = FillP::kFill >= 0;
   constexpr bool kScatter = FILL && FillP::kScatter;
   constexpr bool kSmall = FillP::kSmall;
+  constexpr bool kPerm = FillP::kPerm;
   static_assert(!kSmall || (BATCH && !RT && !FILL), "SMALL is a batch mode of its own");
+  static_assert(!kPerm || (BATCH && REGEN && !RT && !FILL), "PERM is a batch regenerate mode of its own");
   using S = SynShape<K, N, WV>;
   using P = typename S::P;
   constexpr bool kPrio = S::kPrio;
@@ -601,12 +611,12 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     auto erased_of = [&](int m) -> int { return (int)s_ld_u8(BATCH ? pl->erased : a.erased, m); };
     // the LDS point this wave zeroes and (regenerate) stores: an erased point,
     // or RT regenerate's row slot K + wave
-    const int my_erased = RT ? K + wave : (wave < S::kM ? erased_of(wave) : 0);
+    const int my_erased = RT ? K + wave : kPerm ? K : (wave < S::kM ? erased_of(wave) : 0);
     Plane16 Ps[RT ? S::kLoadPer : 1];  // RT: this wave's slots, kept for phase 2
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
     syn_prio<1, kPrio>();
     {
-      if (wave < S::kM && (!RT || REGEN) && !FILL) {
+      if (wave < S::kM && (!RT || REGEN) && !FILL && (!kPerm || wave == 0)) {
         const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int g = 0; g < 4; ++g) L.put(4 * my_erased + g, z);
@@ -750,6 +760,18 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       // (its own stage-1 slots in, LDS XOR atomics out; survivors sorted by point)
       syn_scatter_fill<WV, FillP, 0>(wave, L);
       if (!kLateLoad) prefetch(tile + t_step);
+    } else if constexpr (kPerm) {
+      // ---- 2 (PERM). wave w's four points' share of P(K + t'), read through
+      // the permutation c -> c ^ t', into slot K (zeroed in stage 1)
+      const uint32_t tp = (uint32_t)erased_of(0) ^ (uint32_t)K;
+      struct PermIn {
+        const SynLds &L;
+        uint32_t tp;
+        __device__ __forceinline__ u32x4 operator()(int g) const { return L(4 * (int)((uint32_t)(g >> 2) ^ tp) + (g & 3)); }
+      } in{L, tp};
+      uint32_t acc[16];
+      FillP::part(wave, in, acc);
+      lds_xor_point(L, K, *reinterpret_cast<const Plane16 *>(acc));
     } else if constexpr (kSmall) {
       // ---- 2 (SMALL). the MS checks over A, then the MS x MS recovery
       const uint32_t nrec = s_ld(&pl->nrec);
@@ -861,7 +883,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       // (RT: row w's slot K + w, for w < the tile's rows)
       if constexpr (RT) prefetch(tile + t_step);
       if constexpr (BATCH) {
-        if (RT ? (uint32_t)wave < rt_rows : wave < S::kM) {
+        if (RT ? (uint32_t)wave < rt_rows : kPerm ? wave == 0 : wave < S::kM) {
           uint32_t Pl[16], W[16];
           syn_get_point(L, my_erased, Pl);
 #pragma unroll

@@ -1454,8 +1454,13 @@ struct BatchObjInfo {
   uint16_t rows;    // RT rows: restore, its erased points below k; regenerate, its targets
   uint8_t route;
   uint8_t parts;    // RT descriptors (regenerate: rows in groups of at most n - k)
-  uint8_t ms;       // kRouteSyn: SMALL ms (1, 2) over 0..k+ms-1, or 0 = the N = k + k/4 kernel
+  uint8_t ms;       // kRouteSyn: SMALL ms (1, 2) over 0..k+ms-1, kMsPerm, or 0 = the N = k + k/4 kernel
+  uint16_t target;  // kMsPerm: the one target
 };
+
+// (BatchObjInfo::ms of the PERM regenerate: survivors exactly 0..k-1, one
+// target in k..2k-1)
+constexpr uint8_t kMsPerm = 3;
 
 // The SMALL batch kernels (VDS_EC_SMALL=0 routes their objects to the
 // N = k + k/4 syndrome kernel instead: A/B).
@@ -1503,9 +1508,11 @@ struct SynBatchBuild {
   uint32_t k, n;
   bool regen = false;
   // plans [0, cls_end[0]) are SMALL ms = 1, [cls_end[0], cls_end[1]) ms = 2,
-  // the rest the N = k + k/4 syndrome kernel's (batch_begin resolves them in
-  // that order); each class is one launch over its plans' tiles
-  uint32_t cls_end[2] = {0, 0};
+  // [cls_end[1], cls_end[2]) PERM, the rest the N = k + k/4 syndrome
+  // kernel's (batch_begin resolves them in that order); each class is one
+  // launch over its plans' tiles
+  uint32_t cls_end[3] = {0, 0, 0};
+  uint32_t perm_idx[64];  // PERM plan of target t (k <= t < 2k), or UINT32_MAX
   ParamSlot *slot = nullptr;
   size_t cap_objs = 0, cap_tiles = 0, cap_plans = 0, o_tiles = 0, o_plans = 0;
   SynBatchObj *objs = nullptr;
@@ -1541,11 +1548,22 @@ struct SynBatchBuild {
     hkey.assign(1ull << bits, 0);
     hval.assign(1ull << bits, 0);
     hshift = 64 - bits;
+    for (uint32_t &x : perm_idx) x = UINT32_MAX;
   }
   // The plan of survivor set `seen` (UINT32_MAX: no solve; not for distinct
   // points); ms > 0: the SMALL plan over 0..k+ms-1 (a set always resolves to
   // the same ms within a call: the route is a function of the set).
-  uint32_t plan_of(uint64_t seen, uint32_t ms = 0) {
+  uint32_t plan_of(uint64_t seen, uint32_t ms = 0, uint32_t target = 0) {
+    if (ms == kMsPerm) {  // survivors 0..k-1, one target t in k..2k-1: a plan per t
+      if (target < k || target >= 2 * k || target >= 64) return UINT32_MAX;
+      if (perm_idx[target] != UINT32_MAX) return perm_idx[target];
+      SynBatchPlan pl{};
+      for (uint32_t j = 0; j < k; ++j) pl.point[j] = (uint8_t)j;
+      for (uint32_t i = 0; i < kMaxFastK / 4; ++i) pl.erased[i] = (uint8_t)target;
+      perm_idx[target] = (uint32_t)plans.size();
+      plans.push_back(pl);
+      return perm_idx[target];
+    }
     const size_t mask = hkey.size() - 1;
     size_t i = (size_t)((seen * 0x9E3779B97F4A7C15ull) >> hshift);
     while (hkey[i] != 0 && hkey[i] != seen) i = (i + 1) & mask;
@@ -1614,16 +1632,17 @@ struct SynBatchBuild {
       sa.plans = reinterpret_cast<const SynBatchPlan *>(slot->d + o_plans);
       const SynBatchTile *dt = reinterpret_cast<const SynBatchTile *>(slot->d + o_tiles);
       // one launch per class, over its plans' contiguous tile range
-      const uint32_t bound[3] = {cls_end[0], cls_end[1], (uint32_t)plans.size()};
+      const uint32_t bound[4] = {cls_end[0], cls_end[1], cls_end[2], (uint32_t)plans.size()};
       uint32_t p0 = 0;
-      for (int c = 0; c < 3 && e == hipSuccess; ++c) {
+      for (int c = 0; c < 4 && e == hipSuccess; ++c) {
         const uint64_t t0 = first[p0], t1 = first[bound[c]];
         p0 = bound[c];
         if (t1 == t0) continue;
         sa.tiles = dt + t0;
         sa.total_tiles = (uint32_t)(t1 - t0);
         e = c < 2 ? launch_restore_small_batch(k, (uint32_t)c + 1, sa, s, regen)
-                  : launch_restore_syn_batch(k, n, sa, s, regen);
+            : c == 2 ? (regen ? launch_regen_perm_batch(k, sa, s) : hipErrorInvalidValue)
+                     : launch_restore_syn_batch(k, n, sa, s, regen);
       }
       // (reads the same tables, so before the slot is released)
       if (e == hipSuccess && regen) e = launch_regen_tail_batch(k, n - k, sa.objs, sa.plans, nobj, s);
@@ -1799,16 +1818,16 @@ int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, Syn
     plan.assign(info.size(), 0);
     // SMALL ms = 1 plans first, then ms = 2, then the N = k + k/4 kernel's
     // (SynBatchBuild::cls_end)
-    const uint8_t order[3] = {1, 2, 0};
-    for (int c = 0; c < 3; ++c) {
+    const uint8_t order[4] = {1, 2, kMsPerm, 0};
+    for (int c = 0; c < 4; ++c) {
       for (uint32_t o = 0; o < info.size(); ++o)
         if (info[o].route == kRouteSyn && info[o].ms == order[c] &&
-            (plan[o] = bb.plan_of(info[o].seen, info[o].ms)) == UINT32_MAX) {
+            (plan[o] = bb.plan_of(info[o].seen, info[o].ms, info[o].target)) == UINT32_MAX) {
           bb.abandon(s);
           if (ix.nrt) rb.abandon(s);
           return VDS_EC_ESINGULAR;
         }
-      if (c < 2) bb.cls_end[c] = (uint32_t)bb.plans.size();
+      if (c < 3) bb.cls_end[c] = (uint32_t)bb.plans.size();
     }
   }
   return VDS_EC_OK;
@@ -1962,7 +1981,11 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
           if (ok) hit |= 1ull << t;
         }
       }
-      if (ok) {
+      if (small_enabled() && fits && nt == 1 && (k == 16 || k == 32) && maxid < k && tg[0] >= k && tg[0] < 2 * k) {
+        f.route = kRouteSyn;  // survivors exactly 0..k-1 (k distinct ids below k), one target in k..2k-1
+        f.ms = kMsPerm;
+        f.target = tg[0];
+      } else if (ok) {
         f.route = kRouteSyn;
         f.ms = small_ms_for(k, std::max(maxid, tmax));  // (every target an erased point of 0..k+ms-1)
       } else if (batch_ok && fits && maxid < 256 && tmax < 256) {
@@ -1996,11 +2019,15 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
       uint8_t *const *os = outs + (uint64_t)o * nt;
       if (f.route == kRouteSyn) {
         SynBatchObj &d = bb.fill(ix.syn[o], f.seen, nd, ch, plan[o], f.halves);
-        const uint32_t np = f.ms ? k + f.ms : n;  // the plan's points
-        const uint64_t erased = ~f.seen & ((1ull << np) - 1);
         std::memset(d.regen, 0, sizeof d.regen);
-        for (uint32_t i = 0; i < nt; ++i)
-          d.regen[__builtin_popcountll(erased & ((1ull << tg[i]) - 1))] = os[i];
+        if (f.ms == kMsPerm) {
+          d.regen[0] = os[0];  // (the plan's erased[0] is the target)
+        } else {
+          const uint32_t np = f.ms ? k + f.ms : n;  // the plan's points
+          const uint64_t erased = ~f.seen & ((1ull << np) - 1);
+          for (uint32_t i = 0; i < nt; ++i)
+            d.regen[__builtin_popcountll(erased & ((1ull << tg[i]) - 1))] = os[i];
+        }
         d.out = nullptr;
         d.out_len = 0;
         d.chunk_len = chunk_sizes[o];

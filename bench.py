@@ -191,6 +191,61 @@ def max_over_ranks(values, dist, device):
     return [float(x) for x in t.tolist()]
 
 
+def save_temp_leg(torch, chunk, dev, stream, inp, objects, size, k, n, L, Ls, timed, gib, batches=8):
+    """save_temp (dht_network_client.cpp:74-104): encode replicas 0..n-1 of an
+    object and name each by its SHA-256.  The encode is memory-bound and the
+    hash VALU-bound, so batch b's hashes run on a second stream beside batch
+    b+1's encode (replicas object-major here, [objects][n][Ls], so a batch's
+    n x objects/batches messages are one strided launch).  Reported: the
+    pipelined rate, the same work serial on one stream, and the digests
+    checked against hashlib."""
+    import hashlib
+    rep = torch.empty(objects * n * Ls, dtype=torch.uint8, device=dev)
+    dig = torch.empty(objects * n * 32, dtype=torch.uint8, device=dev)
+    per = objects // batches
+    s2 = torch.cuda.Stream(dev)
+    evs = [torch.cuda.Event() for _ in range(batches)]
+    done = torch.cuda.Event()
+    b0 = rep.data_ptr()
+
+    def enc(o0, cnt, st):
+        chunk.encode_device(k, list(range(n)), inp[o0 * size:], size, size, cnt,
+                            [b0 + (o0 * n + i) * Ls for i in range(n)], n * Ls, stream=st)
+
+    def sha(o0, cnt, st):
+        chunk.sha256_device(rep[o0 * n * Ls:], L, Ls, cnt * n, dig[o0 * n * 32:], st)
+
+    def serial():
+        enc(0, objects, stream)
+        sha(0, objects, stream)
+
+    def pipelined():
+        s2.wait_stream(stream)
+        for b in range(batches):
+            o0 = b * per
+            cnt = per if b + 1 < batches else objects - o0
+            enc(o0, cnt, stream)
+            evs[b].record(stream)
+            s2.wait_event(evs[b])
+            sha(o0, cnt, s2)
+        done.record(s2)
+        stream.wait_event(done)  # (the timed region ends on `stream` after the last hash)
+
+    with torch.cuda.stream(stream):
+        ser_wall, ser_gpu = timed(serial)
+        pip_wall, pip_gpu = timed(pipelined)
+    torch.cuda.synchronize(dev)
+    hb = rep[:(2 * n) * Ls].cpu().numpy().tobytes()
+    dg = dig[:(2 * n) * 32].cpu().numpy().tobytes()
+    assert all(hashlib.sha256(hb[i * Ls:i * Ls + L]).digest() == dg[32 * i:32 * (i + 1)] for i in range(2 * n)), \
+        "save_temp sha"
+    del rep, dig
+    return {"save_temp_GiBps": gib(objects * size, pip_gpu), "serial_GiBps": gib(objects * size, ser_gpu),
+            "batches": batches, "layout": "replicas object-major [objects][n][Ls]",
+            "what": "encode of replicas 0..n-1 + SHA-256 of each, batch b's hashes on a second stream "
+                    "beside batch b+1's encode"}
+
+
 def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02, 0.25), seed=1, align=256):
     """The production shape beside the metric (never in it): MIN_HORCRUX 32,
     GENERATE_HORCRUX 64 (dht_network.h:22-25) on the web client's 64 KiB
@@ -261,6 +316,7 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02
     dg = digests[: 4 * 32].cpu().numpy().tobytes()
     assert all(hashlib.sha256(hb[i * Ls:i * Ls + L]).digest() == dg[32 * i:32 * (i + 1)] for i in range(4)), "sha"
     del digests
+    res["save_temp"] = save_temp_leg(torch, chunk, dev, stream, inp, objects, size, k, n, L, Ls, timed, gib)
     base = np.asarray(rep_ptrs, dtype=np.uint64)
     reps2d = reps.view(n, objects, Ls)
 

@@ -198,6 +198,22 @@ int vds_ec_restore16_host_batch(uint16_t k, const uint16_t *nodes, const uint8_t
                                 const uint64_t *chunk_sizes, uint32_t count, uint8_t *const *outs, uint64_t *out_sizes,
                                 unsigned flags, int max_devices);
 
+/* Caller-owned pinned memory for the host batches (the
+ * path starts and ends in host memory).  vds_ec_host_alloc returns
+ * page-locked, device-mapped memory usable from every device;
+ * vds_ec_host_register pins (and maps) a caller's existing range for as long
+ * as it stays registered.  When a host batch group's objects -- or replicas,
+ * survivors, restored objects -- lie back to back in one such range (the
+ * slab layouts: objects [count][size], replicas [count][n][L], survivors
+ * [count][k][chunk_size], restored objects [count][E]), the H2D DMA reads the
+ * caller's bytes and the results are written into the caller's pages by the
+ * device: no staging copies in host memory.  Anything else is staged as
+ * before.  Free / unregister only when no call using the range is running. */
+int vds_ec_host_alloc(uint64_t bytes, void **ptr);
+int vds_ec_host_free(void *ptr);
+int vds_ec_host_register(void *ptr, uint64_t bytes);
+int vds_ec_host_unregister(void *ptr);
+
 /* ---------------------------------------------------- stripe-range split
  * One object split by stripe range [t0, t1), e.g. over GPUs.
  * Cell t of every replica depends on stripe t alone, so the ranges are

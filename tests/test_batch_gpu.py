@@ -263,3 +263,47 @@ def test_host_contexts_reused_across_threads(gpu):
     _lib.lib().vds_ec_host_ctx_stats(ctypes.byref(created), ctypes.byref(pooled))
     assert created.value <= before + 1, (before, created.value)
     assert pooled.value >= 1
+
+
+@pytest.mark.parametrize("k", [16, 32])
+def test_batch_small_perm_many_tiles(gpu, k):
+    """More tiles than the launch has workgroups (each workgroup walks several
+    tiles, so the next tile's survivors must be prefetched on every route):
+    the SMALL ms = 1 / 2 restore and regenerate and the PERM regenerate over
+    one tile per object, 700 objects, codewords checked against the encode."""
+    import torch
+    from vds_amd import chunk
+    n = 2 * k
+    size = 2048 * 2 * k  # one tile per object
+    count = 700
+    L = chunk.replica_size(k, size)
+    inp = torch.empty(count * size, dtype=torch.uint8, device="cuda")
+    chunk.fill_splitmix_device(inp, count * size, SEED + 31 * k)
+    reps = torch.empty((n, count * L), dtype=torch.uint8, device="cuda")
+    chunk.encode_device(k, list(range(n)), inp, size, size, count, [reps[i].data_ptr() for i in range(n)], L)
+    rng = np.random.default_rng(k)
+    nodes, targets = [], []
+    for o in range(count):
+        kind = o % 4
+        if kind == 0:    # survivors 0..k-1: restore skips phase 2, regenerate is PERM
+            nd, t = list(range(k)), int(rng.integers(k, n))
+        elif kind == 1:  # SMALL ms = 1
+            e = int(rng.integers(0, k))
+            nd, t = [r for r in range(k + 1) if r != e], e
+        else:            # SMALL ms = 2
+            e = sorted(rng.choice(k + 2, 2, replace=False).tolist())
+            nd, t = [r for r in range(k + 2) if r not in e], e[0]
+        if o % 3 == 0:
+            nd = list(rng.permutation(nd))
+        nodes.append(nd)
+        targets.append([t])
+    chunks = [[reps[r].data_ptr() + o * L for r in nd] for o, nd in enumerate(nodes)]
+    out = torch.zeros(count * size, dtype=torch.uint8, device="cuda")
+    chunk.restore_batch_device(k, nodes, chunks, [L] * count, [0] * count,
+                               [out.data_ptr() + o * size for o in range(count)])
+    rg = torch.zeros(count * L, dtype=torch.uint8, device="cuda")
+    chunk.regenerate_batch_device(k, nodes, chunks, [L] * count, targets, [[rg.data_ptr() + o * L] for o in range(count)])
+    torch.cuda.synchronize()
+    assert torch.equal(out, inp)
+    want = torch.stack([reps[targets[o][0], o * L:(o + 1) * L] for o in range(count)])
+    assert torch.equal(rg.view(count, L), want)

@@ -56,6 +56,10 @@ SIGNATURES = {
     "vds_ec_encode8_host": (C.c_int, [C.c_uint8, u8p, C.c_uint32, C.c_void_p, C.c_uint64, vpp, C.c_uint]),
     "vds_ec_restore16_host": (C.c_int, [C.c_uint16, u16p, vpp, C.c_uint64, C.c_void_p, u64p, C.c_uint]),
     "vds_ec_restore8_host": (C.c_int, [C.c_uint8, u8p, vpp, C.c_uint64, C.c_void_p, u64p, C.c_uint]),
+    "vds_ec_host_alloc": (C.c_int, [C.c_uint64, C.POINTER(C.c_void_p)]),
+    "vds_ec_host_free": (C.c_int, [C.c_void_p]),
+    "vds_ec_host_register": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "vds_ec_host_unregister": (C.c_int, [C.c_void_p]),
     "vds_ec_encode16_host_batch": (C.c_int, [C.c_uint16, u16p, C.c_uint32, vpp, u64p, C.c_uint32, vpp,
                                              C.c_uint, C.c_int]),
     "vds_ec_restore16_host_batch": (C.c_int, [C.c_uint16, u16p, vpp, u64p, C.c_uint32, vpp, u64p, C.c_uint, C.c_int]),

@@ -772,6 +772,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       uint32_t acc[16];
       FillP::part(wave, in, acc);
       lds_xor_point(L, K, *reinterpret_cast<const Plane16 *>(acc));
+      if (!kLateLoad) prefetch(tile + t_step);  // (regenerate: the next tile's survivors now)
     } else if constexpr (kSmall) {
       // ---- 2 (SMALL). the MS checks over A, then the MS x MS recovery
       const uint32_t nrec = s_ld(&pl->nrec);
@@ -820,6 +821,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
             *(lds_v4 *)dst = u32x4{o[0], o[1], o[2], o[3]};
         }
       }
+      if (!kLateLoad) prefetch(tile + t_step);  // (regenerate: the next tile's survivors now)
     } else if constexpr (FILL) {
       if (wave < FillP::kFill) {
         uint32_t acc[16];

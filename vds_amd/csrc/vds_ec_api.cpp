@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -2056,6 +2057,41 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
   return VDS_EC_OK;
 }
 
+// ---------------------------------------------- caller-pinned host memory
+// Buffers the caller allocated with vds_ec_host_alloc or registered with
+// vds_ec_host_register (page-locked, mapped, portable across devices).  A
+// host batch whose group of objects (or replicas) lies in one such range as
+// one contiguous slab skips the staging copies: the H2D DMA reads the
+// caller's bytes, and the push kernel writes the results straight into the
+// caller's pages.  Lookups are per group, not per object.
+struct PinnedRange {
+  uint64_t bytes;
+  uint8_t *dev;  // the device address of the range's first byte
+  bool owned;    // vds_ec_host_alloc (freed by vds_ec_host_free) vs registered
+};
+struct PinnedRegistry {
+  std::mutex mu;
+  std::map<uintptr_t, PinnedRange> ranges;  // by start address
+};
+PinnedRegistry &pinned_registry() {
+  static PinnedRegistry *r = new PinnedRegistry();  // never freed: outlives every caller
+  return *r;
+}
+// The device address of host bytes [p, p + len) when they lie in one pinned
+// range, else nullptr.
+uint8_t *pinned_device_ptr(const void *p, uint64_t len) {
+  if (!p) return nullptr;
+  PinnedRegistry &r = pinned_registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (r.ranges.empty()) return nullptr;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  auto it = r.ranges.upper_bound(a);
+  if (it == r.ranges.begin()) return nullptr;
+  --it;
+  if (a + len > it->first + it->second.bytes) return nullptr;
+  return it->second.dev + (a - it->first);
+}
+
 // ------------------------------------------------- multi-GPU host batch
 // Host-resident objects, many per launch: runs of consecutive objects of one
 // size are packed into groups of up to kGroupBytes of input, and the groups
@@ -2076,27 +2112,48 @@ struct BatchSlot {
   size_t in_cap = 0, out_cap = 0;
   bool busy = false;
   std::vector<Copy> out_parts;  // the scatter of h_out once the stream is done
+  size_t d_in_cap = 0, d_out_cap = 0;
+  // pinned host staging of at least in_b / out_b bytes (1 when the group's
+  // caller slabs are pinned and nothing is staged)
   int reserve(size_t in_b, size_t out_b) {
     if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VDS_EC_ENODEV;
     in_b = std::max<size_t>(in_b, 1);
     out_b = std::max<size_t>(out_b, 1);
     if (in_b > in_cap) {
       if (h_in) (void)hipHostFree(h_in);
-      if (d_in) (void)hipFree(d_in);
-      h_in = d_in = nullptr;
+      h_in = nullptr;
       in_cap = 0;
-      if (hipHostMalloc(&h_in, in_b, 0) != hipSuccess || hipMalloc(&d_in, in_b) != hipSuccess) return VDS_EC_ENOMEM;
+      if (hipHostMalloc(&h_in, in_b, 0) != hipSuccess) return VDS_EC_ENOMEM;
       in_cap = in_b;
     }
     if (out_b > out_cap) {
       if (h_out) (void)hipHostFree(h_out);
-      if (d_out) (void)hipFree(d_out);
-      h_out = d_out = h_out_dev = nullptr;
+      h_out = h_out_dev = nullptr;
       out_cap = 0;
-      if (hipHostMalloc(&h_out, out_b, hipHostMallocMapped) != hipSuccess || hipMalloc(&d_out, out_b) != hipSuccess ||
+      if (hipHostMalloc(&h_out, out_b, hipHostMallocMapped) != hipSuccess ||
           hipHostGetDevicePointer(reinterpret_cast<void **>(&h_out_dev), h_out, 0) != hipSuccess)
         return VDS_EC_ENOMEM;
       out_cap = out_b;
+    }
+    return VDS_EC_OK;
+  }
+  // device buffers of at least in_b / out_b bytes
+  int reserve_dev(size_t in_b, size_t out_b) {
+    in_b = std::max<size_t>(in_b, 1);
+    out_b = std::max<size_t>(out_b, 1);
+    if (in_b > d_in_cap) {
+      if (d_in) (void)hipFree(d_in);
+      d_in = nullptr;
+      d_in_cap = 0;
+      if (hipMalloc(&d_in, in_b) != hipSuccess) return VDS_EC_ENOMEM;
+      d_in_cap = in_b;
+    }
+    if (out_b > d_out_cap) {
+      if (d_out) (void)hipFree(d_out);
+      d_out = nullptr;
+      d_out_cap = 0;
+      if (hipMalloc(&d_out, out_b) != hipSuccess) return VDS_EC_ENOMEM;
+      d_out_cap = out_b;
     }
     return VDS_EC_OK;
   }
@@ -2222,12 +2279,26 @@ int encode_host_batch(uint32_t k, const uint16_t *replicas, uint32_t n, const ui
       [&](uint32_t o) { return sizes[o] + (uint64_t)n * vds_ec_replica_size(2, k, sizes[o], flags); });
   return run_host_batch(groups, ndev, [&](BatchSlot &s, const Group &g) -> int {
     const uint64_t size = sizes[g.o0], L = vds_ec_replica_size(2, k, size, flags), m = g.cnt;
-    int rc = s.reserve(m * size, m * n * L);
+    // caller-pinned slabs (vds_ec_host_alloc / _register): no staging copies
+    bool in_slab = size > 0, out_slab = L > 0;
+    for (uint64_t o = 1; o < m && in_slab; ++o) in_slab = objs[g.o0 + o] == objs[g.o0] + o * size;
+    uint8_t *const out0 = outs[(uint64_t)g.o0 * n];
+    for (uint64_t i = 1; i < m * n && out_slab; ++i) out_slab = outs[(uint64_t)g.o0 * n + i] == out0 + i * L;
+    const bool in_direct = in_slab && pinned_device_ptr(objs[g.o0], m * size);
+    uint8_t *const out_dev = out_slab ? pinned_device_ptr(out0, m * n * L) : nullptr;
+    int rc = s.reserve(in_direct ? 1 : m * size, out_dev ? 1 : m * n * L);
     if (rc) return rc;
-    std::vector<Copy> in(m);
-    for (uint64_t o = 0; o < m; ++o) in[o] = {s.h_in + o * size, objs[g.o0 + o], size};
-    parallel_copy(in);
-    hipError_t e = size ? hipMemcpyAsync(s.d_in, s.h_in, m * size, hipMemcpyHostToDevice, s.stream) : hipSuccess;
+    if (!in_direct) {
+      std::vector<Copy> in(m);
+      for (uint64_t o = 0; o < m; ++o) in[o] = {s.h_in + o * size, objs[g.o0 + o], size};
+      parallel_copy(in);
+    }
+    // (the device input buffer, in the staging slot too: sized for the group)
+    rc = s.reserve_dev(m * size, m * n * L);
+    if (rc) return rc;
+    hipError_t e = size ? hipMemcpyAsync(s.d_in, in_direct ? objs[g.o0] : s.h_in, m * size, hipMemcpyHostToDevice,
+                                         s.stream)
+                        : hipSuccess;
     if (e != hipSuccess) return hip_status(e);
     // replica i of the group's object o at d_out + (o n + i) L: the order of
     // outs[], so a caller's slab of replicas is one copy out
@@ -2235,6 +2306,12 @@ int encode_host_batch(uint32_t k, const uint16_t *replicas, uint32_t n, const ui
     for (uint32_t i = 0; i < n; ++i) douts[i] = s.d_out + (uint64_t)i * L;
     rc = encode_device(2, k, replicas, n, s.d_in, size, size, (uint32_t)m, douts.data(), n * L, flags, s.stream);
     if (rc) return rc;
+    if (out_dev) {  // straight into the caller's pinned slab
+      s.out_parts.clear();
+      return hip_status(((reinterpret_cast<uintptr_t>(out_dev) & 15u) == 0)
+                            ? launch_push(out_dev, s.d_out, m * n * L, s.stream)
+                            : hipMemcpyAsync(out0, s.d_out, m * n * L, hipMemcpyDeviceToHost, s.stream));
+    }
     if ((rc = s.push_out(m * n * L))) return rc;
     s.out_parts.resize(m * n);
     for (uint64_t o = 0; o < m; ++o)
@@ -2277,17 +2354,30 @@ int restore_host_batch(uint32_t k, const uint16_t *nodes, const uint8_t *const *
     const uint64_t cs = chunk_sizes[g.o0], m = g.cnt;
     uint64_t cap = 1;
     for (uint64_t o = 0; o < m; ++o) cap = std::max(cap, lens[g.o0 + o]);
-    int rc = s.reserve(m * k * cs, m * cap);
+    // caller-pinned slabs: the survivors as [objects][k][cs], the outputs
+    // back to back at one length
+    const uint8_t *const c0 = chunks[(uint64_t)g.o0 * k];
+    bool in_slab = cs > 0;
+    for (uint64_t i = 1; i < m * k && in_slab; ++i) in_slab = chunks[(uint64_t)g.o0 * k + i] == c0 + i * cs;
+    const bool in_direct = in_slab && pinned_device_ptr(c0, m * k * cs);
+    bool out_slab = cap > 0;
+    for (uint64_t o = 0; o < m && out_slab; ++o)
+      out_slab = lens[g.o0 + o] == cap && outs[g.o0 + o] == outs[g.o0] + o * cap;
+    uint8_t *const out_dev = out_slab ? pinned_device_ptr(outs[g.o0], m * cap) : nullptr;
+    int rc = s.reserve(in_direct ? 1 : m * k * cs, out_dev ? 1 : m * cap);
     if (rc) return rc;
-    std::vector<Copy> in(m * k);
+    rc = s.reserve_dev(m * k * cs, m * cap);
+    if (rc) return rc;
+    std::vector<Copy> in(in_direct ? 0 : m * k);
     std::vector<const uint8_t *> dchunks(m * k);
     for (uint64_t o = 0; o < m; ++o)
       for (uint32_t j = 0; j < k; ++j) {
-        in[o * k + j] = {s.h_in + (o * k + j) * cs, chunks[(g.o0 + o) * k + j], cs};
+        if (!in_direct) in[o * k + j] = {s.h_in + (o * k + j) * cs, chunks[(g.o0 + o) * k + j], cs};
         dchunks[o * k + j] = s.d_in + (o * k + j) * cs;
       }
     parallel_copy(in);
-    hipError_t e = cs ? hipMemcpyAsync(s.d_in, s.h_in, m * k * cs, hipMemcpyHostToDevice, s.stream) : hipSuccess;
+    hipError_t e = cs ? hipMemcpyAsync(s.d_in, in_direct ? c0 : s.h_in, m * k * cs, hipMemcpyHostToDevice, s.stream)
+                      : hipSuccess;
     if (e != hipSuccess) return hip_status(e);
     std::vector<uint64_t> csz(m, cs);
     std::vector<uint8_t *> douts(m);
@@ -2295,8 +2385,12 @@ int restore_host_batch(uint32_t k, const uint16_t *nodes, const uint8_t *const *
     rc = restore_batch_device(k, (uint32_t)m, nodes + (uint64_t)g.o0 * k, dchunks.data(), csz.data(),
                               pads.data() + g.o0, douts.data(), flags, s.stream);
     if (rc) return rc;
-    if ((rc = s.push_out(m * cap))) return rc;
     s.out_parts.clear();
+    if (out_dev)  // straight into the caller's pinned slab
+      return hip_status(((reinterpret_cast<uintptr_t>(out_dev) & 15u) == 0)
+                            ? launch_push(out_dev, s.d_out, m * cap, s.stream)
+                            : hipMemcpyAsync(outs[g.o0], s.d_out, m * cap, hipMemcpyDeviceToHost, s.stream));
+    if ((rc = s.push_out(m * cap))) return rc;
     for (uint64_t o = 0; o < m; ++o)
       if (lens[g.o0 + o]) s.out_parts.push_back({outs[g.o0 + o], s.h_out + o * cap, lens[g.o0 + o]});
     return VDS_EC_OK;
@@ -2383,6 +2477,7 @@ int encode_host_split(uint32_t k, const uint16_t *replicas, uint32_t n, const ui
     const uint64_t in_b = last ? size - sb * t0 : sb * (t1 - t0);
     const uint64_t Lr = 2 * (t1 - t0) + (last && trailer ? 2 : 0);  // replica bytes of the range
     int rc = s.reserve(in_b, n * Lr);
+    if (!rc) rc = s.reserve_dev(in_b, n * Lr);
     if (rc) return rc;
     parallel_copy({{s.h_in, data + sb * t0, in_b}});
     hipError_t e = in_b ? hipMemcpyAsync(s.d_in, s.h_in, in_b, hipMemcpyHostToDevice, s.stream) : hipSuccess;
@@ -2420,6 +2515,7 @@ int restore_host_split(uint32_t k, const uint16_t *nodes, const uint8_t *const *
     const auto [t0, t1] = ranges[g.o0];
     const uint64_t Lr = 2 * (t1 - t0), len = std::min(sb * t1, E) - sb * t0;
     int rc = s.reserve(k * Lr, len);
+    if (!rc) rc = s.reserve_dev(k * Lr, len);
     if (rc) return rc;
     std::vector<Copy> in(k);
     std::vector<const uint8_t *> dchunks(k);
@@ -2646,6 +2742,64 @@ int vds_ec_restore8_host(uint8_t k, const uint8_t *nodes, const uint8_t *const *
   rc = restore_host(1, k, nullptr, m.data(), chunks, chunk_size, len, out, flags);
   if (rc == VDS_EC_OK && out_size) *out_size = len;
   return rc;
+}
+
+int vds_ec_host_alloc(uint64_t bytes, void **ptr) {
+  if (!ptr || bytes == 0) return VDS_EC_EINVAL;
+  *ptr = nullptr;
+  int rc = device_ready();
+  if (rc) return rc;
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) return VDS_EC_ENOMEM;
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipHostFree(p);
+    return VDS_EC_EHIP;
+  }
+  PinnedRegistry &r = pinned_registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  r.ranges[reinterpret_cast<uintptr_t>(p)] = PinnedRange{bytes, static_cast<uint8_t *>(d), true};
+  *ptr = p;
+  return VDS_EC_OK;
+}
+
+int vds_ec_host_free(void *ptr) {
+  if (!ptr) return VDS_EC_OK;
+  PinnedRegistry &r = pinned_registry();
+  {
+    std::lock_guard<std::mutex> g(r.mu);
+    auto it = r.ranges.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == r.ranges.end() || !it->second.owned) return VDS_EC_EINVAL;
+    r.ranges.erase(it);
+  }
+  return hip_status(hipHostFree(ptr));
+}
+
+int vds_ec_host_register(void *ptr, uint64_t bytes) {
+  if (!ptr || bytes == 0) return VDS_EC_EINVAL;
+  int rc = device_ready();
+  if (rc) return rc;
+  if (hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) return VDS_EC_EHIP;
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, ptr, 0) != hipSuccess) {
+    (void)hipHostUnregister(ptr);
+    return VDS_EC_EHIP;
+  }
+  PinnedRegistry &r = pinned_registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  r.ranges[reinterpret_cast<uintptr_t>(ptr)] = PinnedRange{bytes, static_cast<uint8_t *>(d), false};
+  return VDS_EC_OK;
+}
+
+int vds_ec_host_unregister(void *ptr) {
+  PinnedRegistry &r = pinned_registry();
+  {
+    std::lock_guard<std::mutex> g(r.mu);
+    auto it = r.ranges.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == r.ranges.end() || it->second.owned) return VDS_EC_EINVAL;
+    r.ranges.erase(it);
+  }
+  return hip_status(hipHostUnregister(ptr));
 }
 
 int vds_ec_encode16_host_batch(uint16_t k, const uint16_t *replicas, uint32_t n,

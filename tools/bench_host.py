@@ -71,17 +71,30 @@ assert all(g.tobytes() == d.tobytes() for g, d in zip(got, objs))
 gib = a.objects * size / 2**30
 
 
-def live(count, reps):
+def live(count, reps, pinned=False):
     """The live shape through the C ABI with flat numpy buffers (one pointer
-    per object / replica, no per-object Python arrays)."""
+    per object / replica, no per-object Python arrays).  pinned: the caller's
+    slabs come from vds_ec_host_alloc (objects, replicas, a survivor slab
+    [count][k][L] the download loop would receive into, restored objects), so
+    no staging copies are made."""
     import ctypes as C
     from vds_amd import _lib
     lib = _lib.lib()
     k, n, size = 32, 64, 65536
     L = chunk.replica_size(k, size)
-    objs = rng.integers(0, 256, count * size, dtype=np.uint8)
-    reps_buf = np.ones(count * n * L, dtype=np.uint8)   # caller-owned, pre-faulted
-    out = np.ones(count * size, dtype=np.uint8)
+    keep = []
+
+    def buf(nbytes, fill):
+        if not pinned:
+            return np.full(nbytes, fill, dtype=np.uint8)  # caller-owned, pre-faulted
+        b = chunk.PinnedBuffer(nbytes)
+        keep.append(b)
+        b.array[:] = fill
+        return b.array
+    objs = buf(count * size, 0)
+    objs[:] = rng.integers(0, 256, count * size, dtype=np.uint8)
+    reps_buf = buf(count * n * L, 1)
+    out = buf(count * size, 1)
     obj_ptrs = (np.uint64(objs.ctypes.data) + np.arange(count, dtype=np.uint64) * np.uint64(size))
     rep_ptrs = (np.uint64(reps_buf.ctypes.data) + np.arange(count * n, dtype=np.uint64) * np.uint64(L))
     sizes = np.full(count, size, dtype=np.uint64)
@@ -96,6 +109,13 @@ def live(count, reps):
     chunk_ptrs = (np.uint64(reps_buf.ctypes.data) +
                   (np.arange(count, dtype=np.uint64)[:, None] * np.uint64(n) + nodes.astype(np.uint64)) * np.uint64(L))
     chunk_ptrs = np.ascontiguousarray(chunk_ptrs)
+    if pinned:  # the survivors as the download loop would lay them out: one slab [count][k][L]
+        surv = buf(count * k * L, 0)
+        enc()
+        rv = reps_buf.reshape(count, n, L)
+        surv.reshape(count, k, L)[:] = rv[np.arange(count)[:, None], nodes.astype(np.int64)]
+        chunk_ptrs = np.ascontiguousarray(np.uint64(surv.ctypes.data) + np.arange(count * k, dtype=np.uint64).reshape(
+            count, k) * np.uint64(L))
     csz = np.full(count, L, dtype=np.uint64)
     out_ptrs = (np.uint64(out.ctypes.data) + np.arange(count, dtype=np.uint64) * np.uint64(size))
     caps = np.full(count, size, dtype=np.uint64)
@@ -120,7 +140,9 @@ def live(count, reps):
     tr = best(rest)
     assert np.array_equal(out, objs), "live host restore differs"
     g = count * size / 2**30
-    return {"shape": f"k=32, n=64, {count} x 64 KiB host objects, loss p=0.02", "encode_GiBps": round(g / te, 3),
+    del keep
+    return {"shape": f"k=32, n=64, {count} x 64 KiB host objects, loss p=0.02" + (", caller-pinned slabs" if pinned else ""),
+            "encode_GiBps": round(g / te, 3),
             "repair_GiBps": round(g / tr, 3), "encode_s": round(te, 4), "repair_s": round(tr, 4),
             "pcie_bytes_per_object_encode": size + n * L, "pcie_bytes_per_object_repair": k * L + size}
 
@@ -146,4 +168,5 @@ print(json.dumps({"metric": "host-resident (PCIe-inclusive) encode / repair GiB/
                   "repair_per_object_GiBps": round(gib / best_rep, 3),
                   "encode_s": round(best_enc, 4), "repair_s": round(best_rb, 4),
                   "live": live(a.live, a.reps) if a.live else None,
+                  "live_pinned": live(a.live, a.reps, pinned=True) if a.live else None,
                   "split": split(a.split_mib, a.reps) if a.split_mib else None}), flush=True)

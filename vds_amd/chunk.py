@@ -560,3 +560,39 @@ def encode_host_batch(k: int, replicas: Sequence[int], objects: Sequence, max_de
                                                 sizes.ctypes.data_as(_lib.u64p), len(bufs), optrs, 0,
                                                 max_devices), "encode16_host_batch")
     return [[o[: replica_size(k, b.size)] for o in row] for row, b in zip(outs, bufs)]
+
+
+class PinnedBuffer:
+    """Caller-owned pinned host memory (vds_ec_host_alloc): page-locked,
+    device-mapped.  Host batches whose objects, replicas, survivors or outputs
+    lie back to back in such a buffer read and write it directly (no staging
+    copies).  `.array` is a uint8 numpy view; close() (or del) frees it."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        check(_lib.lib().vds_ec_host_alloc(int(nbytes), C.byref(p)), "host_alloc")
+        self.ptr, self.nbytes = p.value, int(nbytes)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def close(self) -> None:
+        if self.ptr:
+            self.array = None
+            check(_lib.lib().vds_ec_host_free(self.ptr), "host_free")
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 (interpreter teardown)
+            pass
+
+
+def host_register(arr) -> None:
+    """Pin (and map) a caller's contiguous numpy buffer for the host batches
+    (vds_ec_host_register); host_unregister before it is freed."""
+    a = _u8(arr)
+    check(_lib.lib().vds_ec_host_register(a.ctypes.data, a.size), "host_register")
+
+
+def host_unregister(arr) -> None:
+    check(_lib.lib().vds_ec_host_unregister(_u8(arr).ctypes.data), "host_unregister")

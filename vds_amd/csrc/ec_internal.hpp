@@ -111,9 +111,6 @@ struct SynRestoreArgs {
   // requested); the interpolation is skipped
   uint8_t *regen[kMaxFastK / 4];
   uint64_t regen_stride;
-  // workgroups of the launch at most (0: the default, 256 x workgroups per
-  // CU): the batch classes run side by side on shares of the CUs
-  uint32_t grid_cap;
   // batch mode (launch_restore_syn_batch): everything per object from tables
   const struct SynBatchObj *objs;
   const struct SynBatchPlan *plans;
@@ -272,9 +269,6 @@ hipError_t launch_restore_syn_batch(uint32_t k, uint32_t n, const SynRestoreArgs
 // SMALL batch mode over the points 0..k+ms-1 (ms = 1, 2; k = 16, 32): tables as
 // launch_restore_syn_batch, plans with small_mask / nrec.
 bool has_restore_small(uint32_t k, uint32_t ms);
-// Workgroups per CU of the (k, k + k/4) restore kernels (their LDS: 2 at k =
-// 16, 1 at k = 32).
-uint32_t restore_syn_blocks_per_cu(uint32_t k);
 // W[j][a] = v_a a^j of the ms checks over A = {0..k+ms-1}; nullptr if not compiled.
 const uint16_t *restore_small_weights(uint32_t k, uint32_t ms);
 hipError_t launch_restore_small_batch(uint32_t k, uint32_t ms, const SynRestoreArgs &a, hipStream_t s, bool regen);

@@ -61,7 +61,6 @@ static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) 
   uint32_t grid = 256u * (blocks_per_cu > 0 ? blocks_per_cu : 1);
   static const uint32_t over = grid_override("VDS_EC_SYN_GRID");
   if (over) grid = over;
-  if (a.grid_cap && grid > a.grid_cap) grid = a.grid_cap;
   if (grid > a.total_tiles) grid = a.total_tiles;
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL((k_restore_syn<K, N, WV, REGEN, BATCH, RT, FILL>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
@@ -116,12 +115,6 @@ hipError_t launch_restore_syn_batch(uint32_t k, uint32_t n, const SynRestoreArgs
   if (k == 32 && n == 40)
     return regen ? launch_restore_syn_kn<32, 40, 8, true, true>(a, s) : launch_restore_syn_kn<32, 40, 8, false, true>(a, s);
   return hipErrorNotSupported;
-}
-
-uint32_t restore_syn_blocks_per_cu(uint32_t k) {
-  if (k == 16) return (160 * 1024) / SynShape<16, 20, 4>::kLdsBytes;
-  if (k == 32) return (160 * 1024) / SynShape<32, 40, 8>::kLdsBytes;
-  return 1;
 }
 
 bool has_restore_small(uint32_t k, uint32_t ms) { return (k == 16 || k == 32) && (ms == 1 || ms == 2); }

@@ -1501,58 +1501,6 @@ inline bool id_set(uint32_t k, const uint16_t *nd, uint64_t *seen, uint32_t *max
   return !wide || ids_distinct(k, nd);
 }
 
-// Side streams of a device for launches that run beside each other (the
-// batch classes): fork() makes them wait for the caller's stream, join()
-// makes the caller's stream wait for them.  Per device, created once, never
-// freed; one fork at a time (the mutex is held from fork to join).
-struct ForkJoin {
-  static constexpr int kSide = 4;
-  std::mutex mu;
-  hipStream_t side[kSide] = {};
-  hipEvent_t start = nullptr, done[kSide] = {};
-  bool ok = false;
-  hipError_t fork(hipStream_t s) {
-    mu.lock();
-    hipError_t e = hipEventRecord(start, s);
-    for (int i = 0; i < kSide && e == hipSuccess; ++i) e = hipStreamWaitEvent(side[i], start, 0);
-    if (e != hipSuccess) mu.unlock();
-    return e;
-  }
-  hipError_t join(hipStream_t s) {
-    hipError_t e = hipSuccess;
-    for (int i = 0; i < kSide; ++i) {
-      const hipError_t r = hipEventRecord(done[i], side[i]);
-      if (r == hipSuccess) {
-        const hipError_t w = hipStreamWaitEvent(s, done[i], 0);
-        if (e == hipSuccess) e = w;
-      } else if (e == hipSuccess) {
-        e = r;
-      }
-    }
-    mu.unlock();
-    return e;
-  }
-};
-
-ForkJoin *fork_join() {
-  static std::mutex m;
-  static std::vector<ForkJoin *> per_dev;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
-  std::lock_guard<std::mutex> g(m);
-  if ((size_t)dev >= per_dev.size()) per_dev.resize(dev + 1, nullptr);
-  if (!per_dev[dev]) {
-    ForkJoin *f = new ForkJoin();  // never freed: outlives every caller
-    bool ok = hipEventCreateWithFlags(&f->start, hipEventDisableTiming) == hipSuccess;
-    for (int i = 0; i < ForkJoin::kSide && ok; ++i)
-      ok = hipStreamCreateWithFlags(&f->side[i], hipStreamNonBlocking) == hipSuccess &&
-           hipEventCreateWithFlags(&f->done[i], hipEventDisableTiming) == hipSuccess;
-    f->ok = ok;
-    per_dev[dev] = f;
-  }
-  return per_dev[dev]->ok ? per_dev[dev] : nullptr;
-}
-
 // Host-side builder of one k_restore_syn batch launch, written straight into
 // a pinned parameter slot: objs (and the empty object), then tiles, then
 // plans.  plan_of() (serial) resolves survivor sets to plans; fill() writes
@@ -1684,48 +1632,18 @@ struct SynBatchBuild {
       sa.objs = reinterpret_cast<const SynBatchObj *>(slot->d);
       sa.plans = reinterpret_cast<const SynBatchPlan *>(slot->d + o_plans);
       const SynBatchTile *dt = reinterpret_cast<const SynBatchTile *>(slot->d + o_tiles);
-      // one launch per class, over its plans' contiguous tile range; with
-      // more than one class, the launches run side by side on their own
-      // streams, each on a share of the CUs proportional to its work, so no
-      // class waits for another's last tiles (ForkJoin)
+      // one launch per class, over its plans' contiguous tile range
       const uint32_t bound[4] = {cls_end[0], cls_end[1], cls_end[2], (uint32_t)plans.size()};
-      uint64_t t_lo[4], t_hi[4];
-      uint32_t p0 = 0, ncls = 0;
-      double work[4], total_work = 0;
-      for (int c = 0; c < 4; ++c) {
-        t_lo[c] = first[p0];
-        t_hi[c] = first[bound[c]];
+      uint32_t p0 = 0;
+      for (int c = 0; c < 4 && e == hipSuccess; ++c) {
+        const uint64_t t0 = first[p0], t1 = first[bound[c]];
         p0 = bound[c];
-        // relative tile cost per class (measured, live shape k = 32: the N =
-        // k + k/4 syndrome kernel's tiles ~1.5x a SMALL one's)
-        static const double kCost[4] = {1.0, 1.2, 1.0, 1.5};
-        work[c] = (double)(t_hi[c] - t_lo[c]) * kCost[c];
-        total_work += work[c];
-        ncls += t_hi[c] > t_lo[c];
-      }
-      ForkJoin *fj = ncls > 1 ? fork_join() : nullptr;
-      if (fj) e = fj->fork(s);
-      const uint32_t slots = 256u * restore_syn_blocks_per_cu(k);
-      for (int c = 0, used = 0; c < 4 && e == hipSuccess; ++c) {
-        if (t_hi[c] == t_lo[c]) continue;
-        sa.tiles = dt + t_lo[c];
-        sa.total_tiles = (uint32_t)(t_hi[c] - t_lo[c]);
-        sa.grid_cap = 0;
-        hipStream_t cs = s;
-        if (fj) {
-          uint32_t share = (uint32_t)(slots * work[c] / total_work + 0.5);
-          share = std::max<uint32_t>(8, (share + 7) & ~7u);
-          sa.grid_cap = share;
-          cs = fj->side[used++];
-        }
-        e = c < 2 ? launch_restore_small_batch(k, (uint32_t)c + 1, sa, cs, regen)
-            : c == 2 ? (regen ? launch_regen_perm_batch(k, sa, cs) : hipErrorInvalidValue)
-                     : launch_restore_syn_batch(k, n, sa, cs, regen);
-      }
-      sa.grid_cap = 0;
-      if (fj) {
-        const hipError_t je = fj->join(s);
-        if (e == hipSuccess) e = je;
+        if (t1 == t0) continue;
+        sa.tiles = dt + t0;
+        sa.total_tiles = (uint32_t)(t1 - t0);
+        e = c < 2 ? launch_restore_small_batch(k, (uint32_t)c + 1, sa, s, regen)
+            : c == 2 ? (regen ? launch_regen_perm_batch(k, sa, s) : hipErrorInvalidValue)
+                     : launch_restore_syn_batch(k, n, sa, s, regen);
       }
       // (reads the same tables, so before the slot is released)
       if (e == hipSuccess && regen) e = launch_regen_tail_batch(k, n - k, sa.objs, sa.plans, nobj, s);
@@ -2174,16 +2092,6 @@ uint8_t *pinned_device_ptr(const void *p, uint64_t len) {
   return it->second.dev + (a - it->first);
 }
 
-// The D2H of a pinned slab by the push kernel (default) or by the copy
-// engine (VDS_EC_PIN_D2H=dma, A/B).
-bool pinned_d2h_dma() {
-  static const bool dma = [] {
-    const char *v = std::getenv("VDS_EC_PIN_D2H");
-    return v && std::strcmp(v, "dma") == 0;
-  }();
-  return dma;
-}
-
 // ------------------------------------------------- multi-GPU host batch
 // Host-resident objects, many per launch: runs of consecutive objects of one
 // size are packed into groups of up to kGroupBytes of input, and the groups
@@ -2400,7 +2308,7 @@ int encode_host_batch(uint32_t k, const uint16_t *replicas, uint32_t n, const ui
     if (rc) return rc;
     if (out_dev) {  // straight into the caller's pinned slab
       s.out_parts.clear();
-      return hip_status(((reinterpret_cast<uintptr_t>(out_dev) & 15u) == 0 && !pinned_d2h_dma())
+      return hip_status(((reinterpret_cast<uintptr_t>(out_dev) & 15u) == 0)
                             ? launch_push(out_dev, s.d_out, m * n * L, s.stream)
                             : hipMemcpyAsync(out0, s.d_out, m * n * L, hipMemcpyDeviceToHost, s.stream));
     }
@@ -2479,7 +2387,7 @@ int restore_host_batch(uint32_t k, const uint16_t *nodes, const uint8_t *const *
     if (rc) return rc;
     s.out_parts.clear();
     if (out_dev)  // straight into the caller's pinned slab
-      return hip_status(((reinterpret_cast<uintptr_t>(out_dev) & 15u) == 0 && !pinned_d2h_dma())
+      return hip_status(((reinterpret_cast<uintptr_t>(out_dev) & 15u) == 0)
                             ? launch_push(out_dev, s.d_out, m * cap, s.stream)
                             : hipMemcpyAsync(outs[g.o0], s.d_out, m * cap, hipMemcpyDeviceToHost, s.stream));
     if ((rc = s.push_out(m * cap))) return rc;

@@ -243,7 +243,7 @@ static int main_small(int argc, char **argv) {
   std::printf("// GENERATED by tools/xorgen/gen_restore small %d %d %d -- do not edit.\n", K, MS, pb);
   std::printf("// Small-M syndromes over the points 0..%d for k_restore_syn's SMALL batch mode (%d waves).\n", N - 1, WV);
   std::printf("template <> struct SmallSyn<%d, %d> {\n", K, MS);
-  std::printf("  static constexpr bool kSmall = true, kPerm = false;\n  static constexpr int kFill = -1;\n");
+  std::printf("  static constexpr bool kSmall = true, kPerm = false, kMulti = false;\n  static constexpr int kFill = -1;\n");
   std::printf("  static constexpr bool kScatter = false;\n");
   std::printf("  static constexpr int kM = %d, kN = %d, kSynSlot = %d;  // syndrome j in LDS slot kSynSlot + j\n", MS, N, N);
   std::printf("  static constexpr uint16_t kW[%d][%d] = {\n", MS, N);
@@ -305,7 +305,8 @@ static int main_perm(int argc, char **argv) {
   std::printf("// GENERATED by tools/xorgen/gen_restore perm %d %d -- do not edit.\n", K, pb);
   std::printf("// P(K + t') = sum_c l_c(K) y_(c ^ t') for k_restore_syn's PERM batch regenerate (%d waves).\n", WV);
   std::printf("template <> struct PermSyn<%d> {\n", K);
-  std::printf("  static constexpr bool kSmall = false, kPerm = true, kScatter = false;\n  static constexpr int kFill = -1;\n");
+  std::printf("  static constexpr bool kSmall = false, kPerm = true, kScatter = false, kMulti = false;\n");
+  std::printf("  static constexpr int kFill = -1;\n");
   std::printf("  static constexpr uint16_t kL[%d] = {", K);
   for (int c = 0; c < K; ++c) std::printf("0x%04x%s", l[c], c + 1 < K ? ", " : "");
   std::printf("};\n");

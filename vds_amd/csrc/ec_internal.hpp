@@ -193,7 +193,7 @@ struct SynBatchPlan {
     uint16_t small_mask[kSmallMaxM][kSmallMaxM][16];
   };
   uint32_t nrec;  // SMALL: rows recovered (restore: erased points below K; regenerate: MS; 0 = none)
-  uint32_t pad_;
+  uint32_t cls;   // MULTI: the plan's phase 2 (kClsSyn, kClsSmall1, kClsSmall2, kClsPerm; restore_syn.hpp)
 };
 struct SynBatchTile {
   uint32_t obj[2];      // object of each half (an unused half: the batch's empty object)
@@ -275,6 +275,9 @@ hipError_t launch_restore_small_batch(uint32_t k, uint32_t ms, const SynRestoreA
 // PERM batch regenerate (k = 16, 32): survivors exactly 0..k-1, one target
 // t = erased[0] of each plan in k..2k-1.
 hipError_t launch_regen_perm_batch(uint32_t k, const SynRestoreArgs &a, hipStream_t s);
+// MULTI: one launch over tiles of every class, each plan's cls choosing its
+// phase 2 (k = 16, 32).
+hipError_t launch_restore_multi_batch(uint32_t k, const SynRestoreArgs &a, hipStream_t s, bool regen);
 hipError_t launch_regen_generic(const RegenArgs &a, hipStream_t s);
 hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s);
 // Returns hipErrorNotSupported when no bit-sliced instantiation exists for (k, n).

@@ -148,6 +148,16 @@ hipError_t launch_regen_perm_batch(uint32_t k, const SynRestoreArgs &a, hipStrea
   return hipErrorNotSupported;
 }
 
+hipError_t launch_restore_multi_batch(uint32_t k, const SynRestoreArgs &a, hipStream_t s, bool regen) {
+  if (k == 16)
+    return regen ? launch_restore_syn_kn<16, 20, 4, true, true, false, MultiP<16>>(a, s)
+                 : launch_restore_syn_kn<16, 20, 4, false, true, false, MultiP<16>>(a, s);
+  if (k == 32)
+    return regen ? launch_restore_syn_kn<32, 40, 8, true, true, false, MultiP<32>>(a, s)
+                 : launch_restore_syn_kn<32, 40, 8, false, true, false, MultiP<32>>(a, s);
+  return hipErrorNotSupported;
+}
+
 hipError_t launch_restore_rt_batch(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen) {
   if (k == 16 && n == 20)
     return regen ? launch_restore_syn_kn<16, 20, 4, true, true, true>(a, s)

@@ -465,6 +465,21 @@ struct NoFill {
   static constexpr bool kScatter = false;
   static constexpr bool kSmall = false;
   static constexpr bool kPerm = false;
+  static constexpr bool kMulti = false;
+};
+// MULTI (batch only): one launch over the tiles of every class of a batch --
+// the N = K + K/4 syndromes (kClsSyn), SMALL ms = 1, 2 (kClsSmall1/2), PERM
+// (kClsPerm, regenerate) -- each tile's phase 2 chosen by its plan's cls, so
+// no class waits for another launch's last tiles.  (Side-by-side launches of
+// the classes on their own streams and CU shares measured much slower: live
+// repair 1283 -> 823 GiB/s.)
+constexpr uint32_t kClsSyn = 0, kClsSmall1 = 1, kClsSmall2 = 2, kClsPerm = 3;
+template <int K> struct MultiP {
+  static constexpr int kFill = -1;
+  static constexpr bool kScatter = false, kSmall = false, kPerm = false, kMulti = true;
+};
+template <class T> struct TypeTag {
+  using type = T;
 };
 // PERM (batch regenerate only): FillP = PermSyn<K> (generated/permsyn_K.inc).
 // Survivors exactly U = {0..K-1}, one target t = K + t' (t' in U): P(t) =
@@ -491,6 +506,8 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   constexpr bool kScatter = FILL && FillP::kScatter;
   constexpr bool kSmall = FillP::kSmall;
   constexpr bool kPerm = FillP::kPerm;
+  constexpr bool kMulti = FillP::kMulti;
+  static_assert(!kMulti || (BATCH && !RT), "MULTI is a batch mode");
   static_assert(!kSmall || (BATCH && !RT && !FILL), "SMALL is a batch mode of its own");
   static_assert(!kPerm || (BATCH && REGEN && !RT && !FILL), "PERM is a batch regenerate mode of its own");
   using S = SynShape<K, N, WV>;
@@ -611,12 +628,15 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     auto erased_of = [&](int m) -> int { return (int)s_ld_u8(BATCH ? pl->erased : a.erased, m); };
     // the LDS point this wave zeroes and (regenerate) stores: an erased point,
     // or RT regenerate's row slot K + wave
-    const int my_erased = RT ? K + wave : kPerm ? K : (wave < S::kM ? erased_of(wave) : 0);
+    // MULTI: this tile's class (uniform); a PERM tile accumulates in slot K
+    const uint32_t cls = kMulti ? s_ld(&pl->cls) : (kPerm ? kClsPerm : kClsSyn);
+    const bool perm_tile = kPerm || (kMulti && REGEN && cls == kClsPerm);
+    const int my_erased = RT ? K + wave : perm_tile ? K : (wave < S::kM ? erased_of(wave) : 0);
     Plane16 Ps[RT ? S::kLoadPer : 1];  // RT: this wave's slots, kept for phase 2
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
     syn_prio<1, kPrio>();
     {
-      if (wave < S::kM && (!RT || REGEN) && !FILL && (!kPerm || wave == 0)) {
+      if (wave < S::kM && (!RT || REGEN) && !FILL && (!perm_tile || wave == 0)) {
         const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int g = 0; g < 4; ++g) L.put(4 * my_erased + g, z);
@@ -666,6 +686,118 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     st.mark(0);
     __syncthreads();
     st.mark(1);
+    // phase-2 bodies, shared by the single-class kernels and MULTI
+    auto phase_perm = [&](auto tag) {
+      using PF = typename decltype(tag)::type;
+      // ---- 2 (PERM). wave w's four points' share of P(K + t'), read through
+      // the permutation c -> c ^ t', into slot K (zeroed in stage 1)
+      const uint32_t tp = (uint32_t)erased_of(0) ^ (uint32_t)K;
+      struct PermIn {
+        const SynLds &L;
+        uint32_t tp;
+        __device__ __forceinline__ u32x4 operator()(int g) const { return L(4 * (int)((uint32_t)(g >> 2) ^ tp) + (g & 3)); }
+      } in{L, tp};
+      uint32_t acc[16];
+      PF::part(wave, in, acc);
+      lds_xor_point(L, K, *reinterpret_cast<const Plane16 *>(acc));
+      if (!kLateLoad) prefetch(tile + t_step);  // (regenerate: the next tile's survivors now)
+    };
+    auto phase_small = [&](auto tag) {
+      using PF = typename decltype(tag)::type;
+      // ---- 2 (SMALL). the MS checks over A, then the MS x MS recovery
+      const uint32_t nrec = s_ld(&pl->nrec);
+      if (nrec != 0) {
+        {
+          uint32_t acc[16 * PF::kM];
+          PF::part(wave, L, acc);
+#pragma unroll
+          for (int j = 0; j < PF::kM; ++j)
+            lds_xor_point(L, PF::kSynSlot + j, *reinterpret_cast<const Plane16 *>(acc + 16 * j));
+        }
+        st.mark(2);
+        __syncthreads();  // the syndromes are whole
+        st.mark(3);
+        constexpr int PW = 16 / WV;  // planes of each recovered point formed by this wave
+        static_assert(PW == 2 || PW == 4, "plane split: 8 or 4 waves");
+        uint32_t sy[PF::kM][16];
+#pragma unroll
+        for (int j = 0; j < PF::kM; ++j) syn_get_point(L, PF::kSynSlot + j, sy[j]);
+#pragma unroll
+        for (int m = 0; m < PF::kM; ++m) {
+          if ((uint32_t)m >= nrec) break;
+          uint32_t o[PW];
+#pragma unroll
+          for (int i = 0; i < PW; ++i) o[i] = 0u;
+#pragma unroll
+          for (int j = 0; j < PF::kM; ++j) {
+            // this wave's PW masks of R[m][j] (16 bits each, one scalar load)
+            uint64_t mk;
+            if constexpr (PW == 2)
+              mk = s_ld(reinterpret_cast<const uint32_t *>(&pl->small_mask[m][j][PW * wave]));
+            else
+              mk = s_ld(reinterpret_cast<const uint64_t *>(&pl->small_mask[m][j][PW * wave]));
+#pragma unroll
+            for (int i = 0; i < PW; ++i)
+#pragma unroll
+              for (int b = 0; b < 16; ++b) o[i] ^= sy[j][b] & (0u - (uint32_t)((mk >> (16 * i + b)) & 1u));
+          }
+          // planes PW w .. PW w + PW - 1 of point erased[m]: 4 PW bytes of
+          // this lane's 16-byte word of group (PW w) / 4
+          const int e = (int)s_ld_u8(pl->erased, m);
+          lds_char *dst = L.at(4 * e + (PW * wave) / 4) + 4 * ((PW * wave) % 4);
+          if constexpr (PW == 2)
+            *(__attribute__((address_space(3))) u32x2 *)dst = u32x2{o[0], o[1]};
+          else
+            *(lds_v4 *)dst = u32x4{o[0], o[1], o[2], o[3]};
+        }
+      }
+      if (!kLateLoad) prefetch(tile + t_step);  // (regenerate: the next tile's survivors now)
+    };
+    auto phase_syn = [&]() {
+      // ---- 2. wave j holds syndrome S_j whole and scatters its share of every
+      // recovered point, c_e[m] += R[m][j] S_j, into the erased slots (zero since
+      // stage 1) with LDS XOR atomics: T = x^b S_j walks the coefficient bits
+      // once for all M products, and no wave has to gather the syndromes (two
+      // barriers and a park/reload of the syndromes fewer than a gather:
+      // 1384 -> 1525 GiB/s).  The wave-uniform branches measured faster than
+      // their alternatives (512 objects): two separate ifs 1562-1563, masked
+      // v_bitop3 with VGPR masks 1520-1534, against 1573-1577 GiB/s.
+      {
+        Plane16 t;
+        P::syndrome(wave, L, t.p);
+        if (!kLateLoad) prefetch(tile + t_step);
+        st.mark(2);
+        // M <= 4: all products before the barrier (their walk overlaps the
+        // slower waves' syndromes); M = 8: four at a time after it (eight
+        // accumulators would not fit beside the prefetched survivors)
+        constexpr int kMC = S::kM <= 4 ? S::kM : 4;
+        if constexpr (kMC < S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
+#pragma unroll
+        for (int m0 = 0; m0 < S::kM; m0 += kMC) {
+          Plane16 ce[kMC];
+#pragma unroll
+          for (int m = 0; m < kMC; ++m) ce[m] = plane_zero();
+          Plane16 t_copy;  // several chunks walk from the same syndrome
+          Plane16 &tt = kMC < S::kM ? (t_copy = t, t_copy) : t;
+#pragma unroll
+          for (int b = 0; b < 16; b += 2) {
+            const Plane16 t1 = plane_mulx(tt);
+#pragma unroll
+            for (int m = 0; m < kMC; ++m) {
+              const uint32_t sel = BATCH ? s_ld(&pl->solve_sel[m0 + m][b >> 2]) : a.solve_sel[m0 + m][b >> 2];
+              const uint32_t two = (sel >> (8 * (b & 3) + wave)) & 0x101u;
+              rec_pair(ce[m], tt, t1, two);
+            }
+            if (b < 14) tt = plane_mulx(t1);
+          }
+          st.mark(3);
+          if constexpr (kMC == S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
+          st.mark(4);
+#pragma unroll
+          for (int m = 0; m < kMC; ++m) lds_xor_point(L, erased_of(m0 + m), ce[m]);
+        }
+      }
+    };
     uint32_t rt_rows = 0;  // RT: rows of this tile
     if constexpr (RT) {
       // ---- 2'. row m of each half = sum_j coef[m][j] * slot j: every wave
@@ -761,67 +893,19 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       syn_scatter_fill<WV, FillP, 0>(wave, L);
       if (!kLateLoad) prefetch(tile + t_step);
     } else if constexpr (kPerm) {
-      // ---- 2 (PERM). wave w's four points' share of P(K + t'), read through
-      // the permutation c -> c ^ t', into slot K (zeroed in stage 1)
-      const uint32_t tp = (uint32_t)erased_of(0) ^ (uint32_t)K;
-      struct PermIn {
-        const SynLds &L;
-        uint32_t tp;
-        __device__ __forceinline__ u32x4 operator()(int g) const { return L(4 * (int)((uint32_t)(g >> 2) ^ tp) + (g & 3)); }
-      } in{L, tp};
-      uint32_t acc[16];
-      FillP::part(wave, in, acc);
-      lds_xor_point(L, K, *reinterpret_cast<const Plane16 *>(acc));
-      if (!kLateLoad) prefetch(tile + t_step);  // (regenerate: the next tile's survivors now)
+      phase_perm(TypeTag<FillP>{});
     } else if constexpr (kSmall) {
-      // ---- 2 (SMALL). the MS checks over A, then the MS x MS recovery
-      const uint32_t nrec = s_ld(&pl->nrec);
-      if (nrec != 0) {
-        {
-          uint32_t acc[16 * FillP::kM];
-          FillP::part(wave, L, acc);
-#pragma unroll
-          for (int j = 0; j < FillP::kM; ++j)
-            lds_xor_point(L, FillP::kSynSlot + j, *reinterpret_cast<const Plane16 *>(acc + 16 * j));
-        }
-        st.mark(2);
-        __syncthreads();  // the syndromes are whole
-        st.mark(3);
-        constexpr int PW = 16 / WV;  // planes of each recovered point formed by this wave
-        static_assert(PW == 2 || PW == 4, "plane split: 8 or 4 waves");
-        uint32_t sy[FillP::kM][16];
-#pragma unroll
-        for (int j = 0; j < FillP::kM; ++j) syn_get_point(L, FillP::kSynSlot + j, sy[j]);
-#pragma unroll
-        for (int m = 0; m < FillP::kM; ++m) {
-          if ((uint32_t)m >= nrec) break;
-          uint32_t o[PW];
-#pragma unroll
-          for (int i = 0; i < PW; ++i) o[i] = 0u;
-#pragma unroll
-          for (int j = 0; j < FillP::kM; ++j) {
-            // this wave's PW masks of R[m][j] (16 bits each, one scalar load)
-            uint64_t mk;
-            if constexpr (PW == 2)
-              mk = s_ld(reinterpret_cast<const uint32_t *>(&pl->small_mask[m][j][PW * wave]));
-            else
-              mk = s_ld(reinterpret_cast<const uint64_t *>(&pl->small_mask[m][j][PW * wave]));
-#pragma unroll
-            for (int i = 0; i < PW; ++i)
-#pragma unroll
-              for (int b = 0; b < 16; ++b) o[i] ^= sy[j][b] & (0u - (uint32_t)((mk >> (16 * i + b)) & 1u));
-          }
-          // planes PW w .. PW w + PW - 1 of point erased[m]: 4 PW bytes of
-          // this lane's 16-byte word of group (PW w) / 4
-          const int e = (int)s_ld_u8(pl->erased, m);
-          lds_char *dst = L.at(4 * e + (PW * wave) / 4) + 4 * ((PW * wave) % 4);
-          if constexpr (PW == 2)
-            *(__attribute__((address_space(3))) u32x2 *)dst = u32x2{o[0], o[1]};
-          else
-            *(lds_v4 *)dst = u32x4{o[0], o[1], o[2], o[3]};
-        }
+      phase_small(TypeTag<FillP>{});
+    } else if constexpr (kMulti) {
+      if (cls == kClsSmall1) {
+        phase_small(TypeTag<SmallSyn<K, 1>>{});
+      } else if (cls == kClsSmall2) {
+        phase_small(TypeTag<SmallSyn<K, 2>>{});
+      } else if (REGEN && cls == kClsPerm) {
+        if constexpr (REGEN) phase_perm(TypeTag<PermSyn<K>>{});
+      } else {
+        phase_syn();
       }
-      if (!kLateLoad) prefetch(tile + t_step);  // (regenerate: the next tile's survivors now)
     } else if constexpr (FILL) {
       if (wave < FillP::kFill) {
         uint32_t acc[16];
@@ -830,49 +914,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       }
       if (!kLateLoad) prefetch(tile + t_step);
     } else {
-    // ---- 2. wave j holds syndrome S_j whole and scatters its share of every
-    // recovered point, c_e[m] += R[m][j] S_j, into the erased slots (zero since
-    // stage 1) with LDS XOR atomics: T = x^b S_j walks the coefficient bits
-    // once for all M products, and no wave has to gather the syndromes (two
-    // barriers and a park/reload of the syndromes fewer than a gather:
-    // 1384 -> 1525 GiB/s).  The wave-uniform branches measured faster than
-    // their alternatives (512 objects): two separate ifs 1562-1563, masked
-    // v_bitop3 with VGPR masks 1520-1534, against 1573-1577 GiB/s.
-    {
-      Plane16 t;
-      P::syndrome(wave, L, t.p);
-      if (!kLateLoad) prefetch(tile + t_step);
-      st.mark(2);
-      // M <= 4: all products before the barrier (their walk overlaps the
-      // slower waves' syndromes); M = 8: four at a time after it (eight
-      // accumulators would not fit beside the prefetched survivors)
-      constexpr int kMC = S::kM <= 4 ? S::kM : 4;
-      if constexpr (kMC < S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
-#pragma unroll
-      for (int m0 = 0; m0 < S::kM; m0 += kMC) {
-        Plane16 ce[kMC];
-#pragma unroll
-        for (int m = 0; m < kMC; ++m) ce[m] = plane_zero();
-        Plane16 t_copy;  // several chunks walk from the same syndrome
-        Plane16 &tt = kMC < S::kM ? (t_copy = t, t_copy) : t;
-#pragma unroll
-        for (int b = 0; b < 16; b += 2) {
-          const Plane16 t1 = plane_mulx(tt);
-#pragma unroll
-          for (int m = 0; m < kMC; ++m) {
-            const uint32_t sel = BATCH ? s_ld(&pl->solve_sel[m0 + m][b >> 2]) : a.solve_sel[m0 + m][b >> 2];
-            const uint32_t two = (sel >> (8 * (b & 3) + wave)) & 0x101u;
-            rec_pair(ce[m], tt, t1, two);
-          }
-          if (b < 14) tt = plane_mulx(t1);
-        }
-        st.mark(3);
-        if constexpr (kMC == S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
-        st.mark(4);
-#pragma unroll
-        for (int m = 0; m < kMC; ++m) lds_xor_point(L, erased_of(m0 + m), ce[m]);
-      }
-    }
+      phase_syn();
     }  // (phase 2)
     st.mark(5);
     __syncthreads();
@@ -885,7 +927,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       // (RT: row w's slot K + w, for w < the tile's rows)
       if constexpr (RT) prefetch(tile + t_step);
       if constexpr (BATCH) {
-        if (RT ? (uint32_t)wave < rt_rows : kPerm ? wave == 0 : wave < S::kM) {
+        if (RT ? (uint32_t)wave < rt_rows : perm_tile ? wave == 0 : wave < S::kM) {
           uint32_t Pl[16], W[16];
           syn_get_point(L, my_erased, Pl);
 #pragma unroll

@@ -1561,6 +1561,7 @@ struct SynBatchBuild {
       SynBatchPlan pl{};
       for (uint32_t j = 0; j < k; ++j) pl.point[j] = (uint8_t)j;
       for (uint32_t i = 0; i < kMaxFastK / 4; ++i) pl.erased[i] = (uint8_t)target;
+      pl.cls = 3;  // (kClsPerm)
       perm_idx[target] = (uint32_t)plans.size();
       plans.push_back(pl);
       return perm_idx[target];
@@ -1572,6 +1573,7 @@ struct SynBatchBuild {
     SynBatchPlan pl;
     if (!syn_plan(k, n, seen, &pl, ms)) return UINT32_MAX;
     if (ms && regen) pl.nrec = ms;  // (regenerate: every erased point of A is a target candidate)
+    pl.cls = ms;                    // (kClsSyn = 0, kClsSmall1 / 2 = ms)
     const uint32_t p = (uint32_t)plans.size();
     plans.push_back(pl);
     hkey[i] = seen;
@@ -1611,15 +1613,28 @@ struct SynBatchBuild {
       (void)param_release(slot, s);
       return VDS_EC_EINVAL;
     }
+    // classes (plans resolved class by class: contiguous plan and tile ranges)
+    const uint32_t bound[4] = {cls_end[0], cls_end[1], cls_end[2], (uint32_t)plans.size()};
+    int ncls = 0;
+    for (int c = 0, q0 = 0; c < 4; q0 = bound[c], ++c) ncls += first[bound[c]] > first[q0];
+    // MULTI (ncls > 1): tile t goes to position pos(t), so that each XCD's
+    // contiguous eighth of the launch (tile_range) gets every eighth tile --
+    // the same mix of classes, whose tiles cost differently
+    const uint64_t R = ntiles;
+    auto pos = [&](uint64_t t) -> uint64_t {
+      if (ncls <= 1) return t;
+      const uint64_t r = t % 8;
+      return r * (R / 8) + std::min<uint64_t>(r, R % 8) + t / 8;
+    };
     SynBatchTile *tiles = reinterpret_cast<SynBatchTile *>(slot->h + o_tiles);
     for (size_t p = 0; p < plans.size(); ++p)
       for (uint64_t t = first[p]; t < first[p + 1]; ++t)
-        tiles[t] = SynBatchTile{{empty, empty}, {0, 0}, (uint32_t)p, 0, 0, 0};
+        tiles[pos(t)] = SynBatchTile{{empty, empty}, {0, 0}, (uint32_t)p, 0, 0, 0};
     for (uint32_t o = 0; o < nobj; ++o) {
       const uint32_t p = obj_plan[o];
       for (uint32_t h = 0; h < obj_halves[o]; ++h) {
         const uint64_t i = used[p]++;
-        SynBatchTile &t = tiles[first[p] + i / 2];
+        SynBatchTile &t = tiles[pos(first[p] + i / 2)];
         t.obj[i & 1] = o;
         t.stripe0[i & 1] = h * kHalfStripes;
         if (regen && h + 1 == obj_halves[o]) t.trailer |= 1u << (i & 1);
@@ -1632,10 +1647,16 @@ struct SynBatchBuild {
       sa.objs = reinterpret_cast<const SynBatchObj *>(slot->d);
       sa.plans = reinterpret_cast<const SynBatchPlan *>(slot->d + o_plans);
       const SynBatchTile *dt = reinterpret_cast<const SynBatchTile *>(slot->d + o_tiles);
-      // one launch per class, over its plans' contiguous tile range
-      const uint32_t bound[4] = {cls_end[0], cls_end[1], cls_end[2], (uint32_t)plans.size()};
+      // one launch: the MULTI kernel over every class's tiles when there is
+      // more than one class (no class waits for another launch's tail), else
+      // the class's own kernel
+      if (ncls > 1) {
+        sa.tiles = dt;
+        sa.total_tiles = (uint32_t)ntiles;
+        e = launch_restore_multi_batch(k, sa, s, regen);
+      }
       uint32_t p0 = 0;
-      for (int c = 0; c < 4 && e == hipSuccess; ++c) {
+      for (int c = 0; c < 4 && e == hipSuccess && ncls == 1; ++c) {
         const uint64_t t0 = first[p0], t1 = first[bound[c]];
         p0 = bound[c];
         if (t1 == t0) continue;

@@ -346,7 +346,7 @@ inline size_t emit_fill_programs(std::string &s, const char *name, int K, const 
   im.map = spoints;
   appendf(s, "struct %s {\n  static constexpr int kFill = %zu;\n  static constexpr bool kScatter = false;\n", name,
           EU.size());
-  appendf(s, "  static constexpr bool kSmall = false, kPerm = false;\n");
+  appendf(s, "  static constexpr bool kSmall = false, kPerm = false, kMulti = false;\n");
   appendf(s, "  static constexpr uint8_t kPoint[%zu] = {", EU.empty() ? (size_t)1 : EU.size());
   for (int e : EU) appendf(s, "%d, ", e);
   appendf(s, "};\n");
@@ -409,7 +409,7 @@ inline size_t emit_fill_scatter(std::string &s, const char *name, int K, const s
     }
   const auto rows = all_bitrows(A, F, K);
   appendf(s, "struct %s {\n  static constexpr int kFill = %d;\n  static constexpr bool kScatter = true;\n", name, F);
-  appendf(s, "  static constexpr bool kSmall = false, kPerm = false;\n");
+  appendf(s, "  static constexpr bool kSmall = false, kPerm = false, kMulti = false;\n");
   appendf(s, "  static constexpr int kParts = %d, kPart = %d;\n", parts, kScatterPart);
   appendf(s, "  static constexpr uint8_t kPoint[%d] = {", F ? F : 1);
   for (int e : EU) appendf(s, "%d, ", e);

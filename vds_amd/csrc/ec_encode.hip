@@ -265,16 +265,23 @@ __device__ __forceinline__ void store_replica_groups(const Plane16 &acc, uint8_t
   transpose16x2(rows, bm);
   // (replica strides L = 2T + 2 leave odd objects 2-byte aligned: gfx950
   // global stores need no natural alignment, tested by the strided batches)
+  // The trailer (trailer0): when group j is its object's last, lane 0 also
+  // writes the object's zero BE16 trailer right after it (cell T = 128
+  // groups_per_obj), instead of a generic launch over every replica of every
+  // object (live shape: 1M two-byte stores, 32 us a launch).
   if constexpr (!STREAM) {  // whole tiles per object: one base, immediate offsets
     uint32_t *b = reinterpret_cast<uint32_t *>(rep + (uint64_t)tp.o * a.out_stride + 256u * tp.q + 4 * lane);
 #pragma unroll
     for (int j = 0; j < 16; ++j) g_st<1>(b + 64 * j, rows[j]);
+    if (a.trailer0 && tp.q + 16 == a.groups_per_obj && lane == 0)
+      *(gmem<uint16_t> *)(rep + (uint64_t)tp.o * a.out_stride + 256u * a.groups_per_obj) = (uint16_t)0;
   } else {
     uint32_t o = tp.o, q = tp.q;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       g_st<1>(rep + (uint64_t)o * a.out_stride + 256u * q + 4 * lane, rows[j]);
       if (++q == a.groups_per_obj) {
+        if (a.trailer0 && lane == 0) *(gmem<uint16_t> *)(rep + (uint64_t)o * a.out_stride + 256u * q) = (uint16_t)0;
         q = 0;
         ++o;
       }

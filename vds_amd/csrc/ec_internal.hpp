@@ -68,6 +68,9 @@ struct FastEncodeArgs {
   uint64_t out_stride;
   uint32_t groups_per_obj;
   uint32_t total_tiles;
+  // 1: also write every replica's trailer -- zero, as the launch covers every
+  // stripe of objects whose size is a multiple of 2k -- at cell T (k >= 8)
+  uint32_t trailer0;
   uint8_t *outs[kMaxLaunchReplicas];  // outs[r] for replica id r = 0..N-1
 };
 

@@ -242,6 +242,9 @@ int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n,
       fa.out_stride = out_stride;
       fa.groups_per_obj = (uint32_t)gpo;
       fa.total_tiles = (uint32_t)total;
+      // every stripe of every object in the launch, size a multiple of 2k:
+      // the zero trailers ride the bit-sliced stores (k >= 8, map 3)
+      fa.trailer0 = (trailer && k >= 8 && 128 * gpo == T && size % stripe_bytes == 0 && total * 16 == gpo * count) ? 1u : 0u;
       for (uint32_t i = 0; i < n; ++i) fa.outs[i] = outs[i];
       hipError_t e = launch_encode_fast(k, n, fa, s);
       if (e != hipSuccess) return hip_status(e);
@@ -255,7 +258,9 @@ int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n,
   struct Part {
     uint64_t o0, cnt, t_begin;
   };
-  Part parts[3] = {{0, o_full, 128 * gpo},
+  const bool trailers_done = fast_groups && trailer && k >= 8 && 128 * gpo == T && size % stripe_bytes == 0 &&
+                             fast_groups == gpo * count;  // (fa.trailer0 above)
+  Part parts[3] = {{0, trailers_done ? 0 : o_full, 128 * gpo},
                    {o_full, o_full < count ? 1u : 0u, fast_groups ? 128 * (fast_groups - o_full * gpo) : 0},
                    {o_full + 1, o_full + 1 < count ? count - o_full - 1 : 0, 0}};
   if (!fast_groups) {

@@ -307,3 +307,24 @@ def test_batch_small_perm_many_tiles(gpu, k):
     assert torch.equal(out, inp)
     want = torch.stack([reps[targets[o][0], o * L:(o + 1) * L] for o in range(count)])
     assert torch.equal(rg.view(count, L), want)
+
+
+@pytest.mark.parametrize("k", [16, 32])
+def test_regenerate_same_set_two_small_sizes(gpu, k):
+    """One survivor set, two objects whose targets route it to SMALL ms = 1
+    (target an erased point below k) and ms = 2 (target k + 1): the plans are
+    per (set, size), not per set."""
+    import torch
+    from vds_amd import chunk
+    n = k + 2
+    size = 1024 * 2 * k
+    nd = [r for r in range(k + 1) if r != 3]  # erased 3 and k + 1 within 0..k+1
+    objs = _objects(torch, k, n, [size, size], seed=4400 + k)
+    targets = [[3], [k + 1]]
+    chunks = [[reps[r].data_ptr() for r in nd] for _, reps in objs]
+    L = objs[0][1][0].numel()
+    outs = [torch.zeros(L + 8, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    chunk.regenerate_batch_device(k, [nd, nd], chunks, [L, L], targets, [[o.data_ptr()] for o in outs])
+    torch.cuda.synchronize()
+    for (host, reps), t, o in zip(objs, targets, outs):
+        assert np.array_equal(o.cpu().numpy()[:L], O.encode(k, t[0], host)), t

@@ -16,6 +16,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -356,8 +357,12 @@ hipError_t param_acquire_n(int cnt, const size_t *bytes, ParamSlot **out) {
   hipError_t e = hipSuccess;
   if (!r->copy && (e = hipStreamCreateWithFlags(&r->copy, hipStreamNonBlocking)) != hipSuccess) return e;
   // per slot, first choice: an idle slot already big enough whose readers are
-  // done (no allocation, no wait); else the next idle slot in rotation; with
-  // fewer than cnt idle slots, take none and wait for a release
+  // done (no allocation, no wait); second: an idle slot big enough whose
+  // readers are still running (the event wait below: the caller is ahead of
+  // the GPU anyway); else the next idle slot in rotation, grown; with fewer
+  // than cnt idle slots, take none and wait for a release.  (Growing a small
+  // slot while a big one is only pending reallocated several MiB of pinned
+  // memory -- milliseconds, synchronising -- on calls of a GPU-bound loop.)
   ParamSlot *sp[ParamRing::kSlots / 2] = {};
   bool pending[ParamRing::kSlots / 2] = {};
   for (;;) {
@@ -367,6 +372,10 @@ hipError_t param_acquire_n(int cnt, const size_t *bytes, ParamSlot **out) {
       for (int i = 0; i < ParamRing::kSlots && !p; ++i) {
         ParamSlot &c = r->slot[(r->next + i) % ParamRing::kSlots];
         if (!c.busy && c.cap >= bytes[got] && (!c.pending || hipEventQuery(c.ev) == hipSuccess)) p = &c;
+      }
+      for (int i = 0; i < ParamRing::kSlots && !p; ++i) {
+        ParamSlot &c = r->slot[(r->next + i) % ParamRing::kSlots];
+        if (!c.busy && c.cap >= bytes[got]) p = &c;
       }
       for (int i = 0; i < ParamRing::kSlots && !p; ++i) {
         ParamSlot &c = r->slot[r->next++ % ParamRing::kSlots];
@@ -1571,17 +1580,20 @@ struct SynBatchBuild {
       plans.push_back(pl);
       return perm_idx[target];
     }
+    // (keyed by set AND ms: a regenerate's route also depends on its targets,
+    // so one set may meet two SMALL sizes in a call)
+    const uint64_t hk = seen | ((uint64_t)ms << 56);
     const size_t mask = hkey.size() - 1;
-    size_t i = (size_t)((seen * 0x9E3779B97F4A7C15ull) >> hshift);
-    while (hkey[i] != 0 && hkey[i] != seen) i = (i + 1) & mask;
-    if (hkey[i] == seen) return hval[i];
+    size_t i = (size_t)((hk * 0x9E3779B97F4A7C15ull) >> hshift);
+    while (hkey[i] != 0 && hkey[i] != hk) i = (i + 1) & mask;
+    if (hkey[i] == hk) return hval[i];
     SynBatchPlan pl;
     if (!syn_plan(k, n, seen, &pl, ms)) return UINT32_MAX;
     if (ms && regen) pl.nrec = ms;  // (regenerate: every erased point of A is a target candidate)
     pl.cls = ms;                    // (kClsSyn = 0, kClsSmall1 / 2 = ms)
     const uint32_t p = (uint32_t)plans.size();
     plans.push_back(pl);
-    hkey[i] = seen;
+    hkey[i] = hk;
     hval[i] = p;
     return p;
   }
@@ -1827,6 +1839,35 @@ struct BatchIndex {
   }
 };
 
+// VDS_EC_HOST_TRACE=1: the batched calls print their host phases (us) to
+// stderr (planning cost study).
+struct HostTrace {
+  const char *name;
+  bool on;
+  std::chrono::steady_clock::time_point t0, last;
+  char buf[256];
+  int len = 0;
+  explicit HostTrace(const char *n) : name(n), on(enabled()) {
+    if (on) t0 = last = std::chrono::steady_clock::now();
+  }
+  static bool enabled() {
+    static const bool e = std::getenv("VDS_EC_HOST_TRACE") != nullptr;
+    return e;
+  }
+  void mark(const char *phase) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    const double us = std::chrono::duration<double, std::micro>(now - last).count();
+    last = now;
+    if (len < (int)sizeof buf - 40) len += std::snprintf(buf + len, sizeof buf - len, " %s=%.0f", phase, us);
+  }
+  ~HostTrace() {
+    if (!on) return;
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    std::fprintf(stderr, "vds_ec host %s:%s total=%.0f us\n", name, buf, us);
+  }
+};
+
 // Acquire both builders' slots (together: see param_acquire_n), resolve the
 // syndrome objects' plans (serial: the plan store and the per-call hash).
 int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, SynBatchBuild &bb, RtBatchBuild &rb,
@@ -1842,20 +1883,93 @@ int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, Syn
   if (ix.nsyn) bb.attach(sl[nb++]);
   if (ix.nrt) rb.attach(sl[nb++]);
   if (ix.nsyn) {
-    plan.assign(info.size(), 0);
-    // SMALL ms = 1 plans first, then ms = 2, then the N = k + k/4 kernel's
-    // (SynBatchBuild::cls_end)
-    const uint8_t order[4] = {1, 2, kMsPerm, 0};
-    for (int c = 0; c < 4; ++c) {
-      for (uint32_t o = 0; o < info.size(); ++o)
-        if (info[o].route == kRouteSyn && info[o].ms == order[c] &&
-            (plan[o] = bb.plan_of(info[o].seen, info[o].ms, info[o].target)) == UINT32_MAX) {
-          bb.abandon(s);
-          if (ix.nrt) rb.abandon(s);
-          return VDS_EC_ESINGULAR;
+    // Plans are per distinct (class, survivor set), and a repair loop's batch
+    // has ~1000 of them over ~16K objects: the distinct keys are found in
+    // parallel, resolved serially in class order (SMALL ms = 1, ms = 2, PERM,
+    // then the N = k + k/4 kernel's: SynBatchBuild::cls_end), and every
+    // object's plan looked up in parallel from the resolved table.
+    // (Resolving object by object, serially, took ~130 us of a ~440 us call.)
+    const uint32_t count = (uint32_t)info.size();
+    auto key_of = [&](const BatchObjInfo &f) -> uint64_t {
+      if (f.ms == kMsPerm) return (1ull << 63) | f.target;
+      return ((uint64_t)f.ms << 56) | f.seen;  // (survivors of the syndrome routes lie below 64 - 8)
+    };
+    auto rank_of = [](uint64_t key) -> int {  // class order
+      if (key >> 63) return 2;
+      const uint32_t ms = (uint32_t)(key >> 56);
+      return ms == 1 ? 0 : ms == 2 ? 1 : 3;
+    };
+    std::mutex mu;
+    std::vector<uint64_t> keys;
+    parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
+      std::vector<uint64_t> local;
+      std::vector<uint64_t> tab(256, 0);  // open addressing, 0 = free (no key is 0: a set has k >= 1 members)
+      size_t used = 0;
+      for (uint32_t o = o0; o < o1; ++o) {
+        if (info[o].route != kRouteSyn) continue;
+        const uint64_t key = key_of(info[o]);
+        if (2 * (used + 1) > tab.size()) {  // grow
+          std::vector<uint64_t> t2(2 * tab.size(), 0);
+          for (uint64_t x : tab)
+            if (x) {
+              size_t i = (size_t)((x * 0x9E3779B97F4A7C15ull) >> 40) & (t2.size() - 1);
+              while (t2[i]) i = (i + 1) & (t2.size() - 1);
+              t2[i] = x;
+            }
+          tab.swap(t2);
         }
-      if (c < 3) bb.cls_end[c] = (uint32_t)bb.plans.size();
+        size_t i = (size_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & (tab.size() - 1);
+        while (tab[i] && tab[i] != key) i = (i + 1) & (tab.size() - 1);
+        if (!tab[i]) {
+          tab[i] = key;
+          ++used;
+          local.push_back(key);
+        }
+      }
+      std::lock_guard<std::mutex> g(mu);
+      keys.insert(keys.end(), local.begin(), local.end());
+    });
+    std::sort(keys.begin(), keys.end(), [&](uint64_t a, uint64_t b) {
+      const int ra = rank_of(a), rb = rank_of(b);
+      return ra != rb ? ra < rb : a < b;
+    });
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    // resolve (serial, per distinct key) into a read-only key -> plan table
+    size_t tsize = 16;
+    while (tsize < 2 * keys.size()) tsize *= 2;
+    std::vector<uint64_t> tkey(tsize, 0);
+    std::vector<uint32_t> tval(tsize, 0);
+    int c = 0;
+    for (uint64_t key : keys) {
+      while (c < rank_of(key)) {
+        if (c < 3) bb.cls_end[c] = (uint32_t)bb.plans.size();
+        ++c;
+      }
+      const bool perm = key >> 63;
+      const uint32_t ms = perm ? kMsPerm : (uint32_t)(key >> 56);
+      const uint64_t seen = perm ? ((1ull << bb.k) - 1) : (key & ((1ull << 56) - 1));
+      const uint32_t p = bb.plan_of(seen, ms, perm ? (uint32_t)(key & 0xFFFF) : 0u);
+      if (p == UINT32_MAX) {
+        bb.abandon(s);
+        if (ix.nrt) rb.abandon(s);
+        return VDS_EC_ESINGULAR;
+      }
+      size_t i = (size_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & (tsize - 1);
+      while (tkey[i]) i = (i + 1) & (tsize - 1);
+      tkey[i] = key;
+      tval[i] = p;
     }
+    for (; c < 3; ++c) bb.cls_end[c] = (uint32_t)bb.plans.size();
+    plan.assign(count, 0);
+    parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
+      for (uint32_t o = o0; o < o1; ++o) {
+        if (info[o].route != kRouteSyn) continue;
+        const uint64_t key = key_of(info[o]);
+        size_t i = (size_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & (tsize - 1);
+        while (tkey[i] != key) i = (i + 1) & (tsize - 1);
+        plan[o] = tval[i];
+      }
+    });
   }
   return VDS_EC_OK;
 }
@@ -1877,6 +1991,7 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
   const uint32_t n = k + k / 4;
   const bool batch_ok = !(flags & VDS_EC_F_CELLS) && k % 4 == 0 && has_restore_syn(k, n);
   const bool syn = batch_ok && !restore_path_override_bs();
+  HostTrace ht("restore_batch");
   // pass 1 (parallel): every object validated before anything is enqueued,
   // its route and sizes
   std::vector<uint64_t> lens(count);
@@ -1919,12 +2034,15 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
   if (err.rc) return err.rc;
   int rc = device_ready();
   if (rc) return rc;
+  ht.mark("pass1");
   BatchIndex ix;
   ix.build(info);
   SynBatchBuild bb{k, n};
   RtBatchBuild rb{k, n};
   std::vector<uint32_t> plan;
+  ht.mark("index");
   if ((rc = batch_begin(info, ix, bb, rb, plan, s))) return rc;
+  ht.mark("begin");
   // pass 2 (parallel): the descriptors
   parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
     for (uint32_t o = o0; o < o1; ++o) {
@@ -1948,7 +2066,9 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
       d->chunk_len = chunk_sizes[o];
     }
   });
+  ht.mark("pass2");
   if ((rc = batch_launch(ix, bb, rb, false, s))) return rc;
+  ht.mark("launch");
   for (uint32_t o = 0; o < count; ++o) {
     if (info[o].route != kRouteOne) continue;
     std::vector<uint16_t> m((size_t)k * k);
@@ -1974,6 +2094,7 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
   const uint32_t n = k + k / 4, R = n - k;
   const bool batch_ok = k % 4 == 0 && has_restore_syn(k, n);
   const bool syn = batch_ok && !restore_path_override_bs();
+  HostTrace ht("regenerate_batch");
   std::vector<BatchObjInfo> info(count);
   FirstError err;
   parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
@@ -2030,13 +2151,16 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
   if (rc) return rc;
   for (const BatchObjInfo &f : info)  // (RT descriptors per object: nt / (n - k) rounded up, < 256)
     if (f.route == kRouteRt && (uint32_t)f.parts * R < nt) return VDS_EC_EINVAL;
+  ht.mark("pass1");
   BatchIndex ix;
   ix.build(info);
   SynBatchBuild bb{k, n};
   bb.regen = true;
   RtBatchBuild rb{k, n};
   std::vector<uint32_t> plan;
+  ht.mark("index");
   if ((rc = batch_begin(info, ix, bb, rb, plan, s))) return rc;
+  ht.mark("begin");
   parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
     for (uint32_t o = o0; o < o1; ++o) {
       const BatchObjInfo &f = info[o];
@@ -2073,7 +2197,9 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
       }
     }
   });
+  ht.mark("pass2");
   if ((rc = batch_launch(ix, bb, rb, true, s))) return rc;
+  ht.mark("launch");
   for (uint32_t o = 0; o < count; ++o) {
     if (info[o].route != kRouteOne) continue;
     rc = regenerate_device(2, k, nodes + (uint64_t)o * k, chunks + (uint64_t)o * k, chunk_sizes[o], 0, 1,

@@ -1381,7 +1381,6 @@ class HostPool {
       std::lock_guard<std::mutex> g(mu_);
       cur_ = job;
       ++gen_;
-      gen_seen_.store(gen_, std::memory_order_release);
     }
     cv_.notify_all();
     work(*job);
@@ -1413,17 +1412,9 @@ class HostPool {
       }
     }
   }
-  // After a job a worker spins for a short while before it sleeps: a batch
-  // call runs several parallel passes back to back, and waking sleeping
-  // workers through the condition variable cost tens of microseconds a pass.
   void loop() {
     uint64_t seen = 0;
     for (;;) {
-      const auto t0 = std::chrono::steady_clock::now();
-      while (gen_seen_.load(std::memory_order_acquire) == seen &&
-             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(300)) {
-        for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
-      }
       std::shared_ptr<Job> j;
       {
         std::unique_lock<std::mutex> g(mu_);
@@ -1438,7 +1429,6 @@ class HostPool {
   std::condition_variable cv_;
   std::shared_ptr<Job> cur_;
   uint64_t gen_ = 0;
-  std::atomic<uint64_t> gen_seen_{0};  // (gen_, for the spinning workers)
   unsigned nworkers_ = 0;
 };
 

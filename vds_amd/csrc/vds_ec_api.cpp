@@ -357,12 +357,11 @@ hipError_t param_acquire_n(int cnt, const size_t *bytes, ParamSlot **out) {
   hipError_t e = hipSuccess;
   if (!r->copy && (e = hipStreamCreateWithFlags(&r->copy, hipStreamNonBlocking)) != hipSuccess) return e;
   // per slot, first choice: an idle slot already big enough whose readers are
-  // done (no allocation, no wait); second: an idle slot big enough whose
-  // readers are still running (the event wait below: the caller is ahead of
-  // the GPU anyway); else the next idle slot in rotation, grown; with fewer
-  // than cnt idle slots, take none and wait for a release.  (Growing a small
-  // slot while a big one is only pending reallocated several MiB of pinned
-  // memory -- milliseconds, synchronising -- on calls of a GPU-bound loop.)
+  // done (no allocation, no wait); else the next idle slot in rotation; with
+  // fewer than cnt idle slots, take none and wait for a release.  (Taking a
+  // big slot whose readers are still running instead of growing another made
+  // every call wait for the previous one's kernels: the host planning no
+  // longer overlapped the GPU, live repair 1020 -> 788 GiB/s.)
   ParamSlot *sp[ParamRing::kSlots / 2] = {};
   bool pending[ParamRing::kSlots / 2] = {};
   for (;;) {
@@ -372,10 +371,6 @@ hipError_t param_acquire_n(int cnt, const size_t *bytes, ParamSlot **out) {
       for (int i = 0; i < ParamRing::kSlots && !p; ++i) {
         ParamSlot &c = r->slot[(r->next + i) % ParamRing::kSlots];
         if (!c.busy && c.cap >= bytes[got] && (!c.pending || hipEventQuery(c.ev) == hipSuccess)) p = &c;
-      }
-      for (int i = 0; i < ParamRing::kSlots && !p; ++i) {
-        ParamSlot &c = r->slot[(r->next + i) % ParamRing::kSlots];
-        if (!c.busy && c.cap >= bytes[got]) p = &c;
       }
       for (int i = 0; i < ParamRing::kSlots && !p; ++i) {
         ParamSlot &c = r->slot[r->next++ % ParamRing::kSlots];
@@ -1883,93 +1878,21 @@ int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, Syn
   if (ix.nsyn) bb.attach(sl[nb++]);
   if (ix.nrt) rb.attach(sl[nb++]);
   if (ix.nsyn) {
-    // Plans are per distinct (class, survivor set), and a repair loop's batch
-    // has ~1000 of them over ~16K objects: the distinct keys are found in
-    // parallel, resolved serially in class order (SMALL ms = 1, ms = 2, PERM,
-    // then the N = k + k/4 kernel's: SynBatchBuild::cls_end), and every
-    // object's plan looked up in parallel from the resolved table.
-    // (Resolving object by object, serially, took ~130 us of a ~440 us call.)
-    const uint32_t count = (uint32_t)info.size();
-    auto key_of = [&](const BatchObjInfo &f) -> uint64_t {
-      if (f.ms == kMsPerm) return (1ull << 63) | f.target;
-      return ((uint64_t)f.ms << 56) | f.seen;  // (survivors of the syndrome routes lie below 64 - 8)
-    };
-    auto rank_of = [](uint64_t key) -> int {  // class order
-      if (key >> 63) return 2;
-      const uint32_t ms = (uint32_t)(key >> 56);
-      return ms == 1 ? 0 : ms == 2 ? 1 : 3;
-    };
-    std::mutex mu;
-    std::vector<uint64_t> keys;
-    parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
-      std::vector<uint64_t> local;
-      std::vector<uint64_t> tab(256, 0);  // open addressing, 0 = free (no key is 0: a set has k >= 1 members)
-      size_t used = 0;
-      for (uint32_t o = o0; o < o1; ++o) {
-        if (info[o].route != kRouteSyn) continue;
-        const uint64_t key = key_of(info[o]);
-        if (2 * (used + 1) > tab.size()) {  // grow
-          std::vector<uint64_t> t2(2 * tab.size(), 0);
-          for (uint64_t x : tab)
-            if (x) {
-              size_t i = (size_t)((x * 0x9E3779B97F4A7C15ull) >> 40) & (t2.size() - 1);
-              while (t2[i]) i = (i + 1) & (t2.size() - 1);
-              t2[i] = x;
-            }
-          tab.swap(t2);
+    plan.assign(info.size(), 0);
+    // SMALL ms = 1 plans first, then ms = 2, then PERM, then the N = k + k/4
+    // kernel's (SynBatchBuild::cls_end).  (Finding the distinct sets in
+    // parallel and resolving each once measured slower: 110 -> 245 us.)
+    const uint8_t order[4] = {1, 2, kMsPerm, 0};
+    for (int c = 0; c < 4; ++c) {
+      for (uint32_t o = 0; o < info.size(); ++o)
+        if (info[o].route == kRouteSyn && info[o].ms == order[c] &&
+            (plan[o] = bb.plan_of(info[o].seen, info[o].ms, info[o].target)) == UINT32_MAX) {
+          bb.abandon(s);
+          if (ix.nrt) rb.abandon(s);
+          return VDS_EC_ESINGULAR;
         }
-        size_t i = (size_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & (tab.size() - 1);
-        while (tab[i] && tab[i] != key) i = (i + 1) & (tab.size() - 1);
-        if (!tab[i]) {
-          tab[i] = key;
-          ++used;
-          local.push_back(key);
-        }
-      }
-      std::lock_guard<std::mutex> g(mu);
-      keys.insert(keys.end(), local.begin(), local.end());
-    });
-    std::sort(keys.begin(), keys.end(), [&](uint64_t a, uint64_t b) {
-      const int ra = rank_of(a), rb = rank_of(b);
-      return ra != rb ? ra < rb : a < b;
-    });
-    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
-    // resolve (serial, per distinct key) into a read-only key -> plan table
-    size_t tsize = 16;
-    while (tsize < 2 * keys.size()) tsize *= 2;
-    std::vector<uint64_t> tkey(tsize, 0);
-    std::vector<uint32_t> tval(tsize, 0);
-    int c = 0;
-    for (uint64_t key : keys) {
-      while (c < rank_of(key)) {
-        if (c < 3) bb.cls_end[c] = (uint32_t)bb.plans.size();
-        ++c;
-      }
-      const bool perm = key >> 63;
-      const uint32_t ms = perm ? kMsPerm : (uint32_t)(key >> 56);
-      const uint64_t seen = perm ? ((1ull << bb.k) - 1) : (key & ((1ull << 56) - 1));
-      const uint32_t p = bb.plan_of(seen, ms, perm ? (uint32_t)(key & 0xFFFF) : 0u);
-      if (p == UINT32_MAX) {
-        bb.abandon(s);
-        if (ix.nrt) rb.abandon(s);
-        return VDS_EC_ESINGULAR;
-      }
-      size_t i = (size_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & (tsize - 1);
-      while (tkey[i]) i = (i + 1) & (tsize - 1);
-      tkey[i] = key;
-      tval[i] = p;
+      if (c < 3) bb.cls_end[c] = (uint32_t)bb.plans.size();
     }
-    for (; c < 3; ++c) bb.cls_end[c] = (uint32_t)bb.plans.size();
-    plan.assign(count, 0);
-    parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
-      for (uint32_t o = o0; o < o1; ++o) {
-        if (info[o].route != kRouteSyn) continue;
-        const uint64_t key = key_of(info[o]);
-        size_t i = (size_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & (tsize - 1);
-        while (tkey[i] != key) i = (i + 1) & (tsize - 1);
-        plan[o] = tval[i];
-      }
-    });
   }
   return VDS_EC_OK;
 }

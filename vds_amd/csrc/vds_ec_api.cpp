@@ -395,13 +395,18 @@ hipError_t param_acquire_n(int cnt, const size_t *bytes, ParamSlot **out) {
     if (e == hipSuccess && !sl.ev) e = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming);
     if (e == hipSuccess && !sl.copied) e = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming);
     if (e == hipSuccess && bytes[i] > sl.cap) {
+      // grown to a power of two (at least 64 KiB): the batch calls' tables
+      // vary a little from call to call, and each growth frees device memory
+      // (hipFree waits for the device) -- a few ms inside a repair loop
+      size_t cap = 64u << 10;
+      while (cap < bytes[i]) cap *= 2;
       if (sl.h) (void)hipHostFree(sl.h);
       if (sl.d) (void)hipFree(sl.d);
       sl.h = sl.d = nullptr;
       sl.cap = 0;
-      e = hipHostMalloc(&sl.h, bytes[i], 0);
-      if (e == hipSuccess) e = hipMalloc(&sl.d, bytes[i]);
-      if (e == hipSuccess) sl.cap = bytes[i];
+      e = hipHostMalloc(&sl.h, cap, 0);
+      if (e == hipSuccess) e = hipMalloc(&sl.d, cap);
+      if (e == hipSuccess) sl.cap = cap;
     }
   }
   if (e != hipSuccess) {  // all of them back, unused (nothing was enqueued on them)
@@ -1878,21 +1883,38 @@ int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, Syn
   if (ix.nsyn) bb.attach(sl[nb++]);
   if (ix.nrt) rb.attach(sl[nb++]);
   if (ix.nsyn) {
-    plan.assign(info.size(), 0);
-    // SMALL ms = 1 plans first, then ms = 2, then PERM, then the N = k + k/4
-    // kernel's (SynBatchBuild::cls_end).  (Finding the distinct sets in
-    // parallel and resolving each once measured slower: 110 -> 245 us.)
-    const uint8_t order[4] = {1, 2, kMsPerm, 0};
-    for (int c = 0; c < 4; ++c) {
-      for (uint32_t o = 0; o < info.size(); ++o)
-        if (info[o].route == kRouteSyn && info[o].ms == order[c] &&
-            (plan[o] = bb.plan_of(info[o].seen, info[o].ms, info[o].target)) == UINT32_MAX) {
-          bb.abandon(s);
-          if (ix.nrt) rb.abandon(s);
-          return VDS_EC_ESINGULAR;
-        }
-      if (c < 3) bb.cls_end[c] = (uint32_t)bb.plans.size();
+    // One pass resolves every object's plan (first seen, first numbered);
+    // then the plans are renumbered class by class -- SMALL ms = 1, ms = 2,
+    // PERM, the N = k + k/4 kernel's (SynBatchBuild::cls_end) -- so each
+    // class's tiles are contiguous.  (Four passes, one per class, cost ~30 us
+    // more at 16K objects; finding the distinct sets in parallel and
+    // resolving each once measured slower still: 110 -> 245 us.)
+    const uint32_t count = (uint32_t)info.size();
+    plan.assign(count, 0);
+    for (uint32_t o = 0; o < count; ++o)
+      if (info[o].route == kRouteSyn &&
+          (plan[o] = bb.plan_of(info[o].seen, info[o].ms, info[o].target)) == UINT32_MAX) {
+        bb.abandon(s);
+        if (ix.nrt) rb.abandon(s);
+        return VDS_EC_ESINGULAR;
+      }
+    const size_t np = bb.plans.size();
+    auto rank = [](uint32_t cls) { return cls == 1 ? 0 : cls == 2 ? 1 : cls == 3 ? 2 : 3; };
+    std::vector<uint32_t> order(np), remap(np);
+    uint32_t cnt[5] = {0, 0, 0, 0, 0};
+    for (size_t p = 0; p < np; ++p) ++cnt[rank(bb.plans[p].cls) + 1];
+    for (int c = 1; c < 5; ++c) cnt[c] += cnt[c - 1];
+    for (int c = 0; c < 3; ++c) bb.cls_end[c] = cnt[c + 1];
+    for (size_t p = 0; p < np; ++p) {
+      const uint32_t q = cnt[rank(bb.plans[p].cls)]++;
+      order[q] = (uint32_t)p;
+      remap[p] = q;
     }
+    std::vector<SynBatchPlan> sorted(np);
+    for (size_t q = 0; q < np; ++q) sorted[q] = bb.plans[order[q]];
+    bb.plans.swap(sorted);
+    for (uint32_t o = 0; o < count; ++o)
+      if (info[o].route == kRouteSyn) plan[o] = remap[plan[o]];
   }
   return VDS_EC_OK;
 }

@@ -80,11 +80,6 @@ constexpr int enc_step_cost(uint32_t c) {
   return (VDS_ENC_PAAR && horner_paar_cost(c) > 0) ? horner_paar_cost(c) : horner_cost((int)c);
 }
 
-// The pairs' combination P(r) = P0(y) + r P1(y) as one Horner step (A/B:
-// VDS_ENC_COMBINE_PAAR=1; default off until measured).
-#ifndef VDS_ENC_COMBINE_PAAR
-#define VDS_ENC_COMBINE_PAAR 0
-#endif
 
 constexpr uint32_t pair_y(int r) { return gf16_mul((uint32_t)r, (uint32_t)r) ^ (uint32_t)r; }
 constexpr int pair_cost(int r) { return 2 * enc_step_cost(pair_y(r)) + 1; }
@@ -500,11 +495,11 @@ __device__ __forceinline__ void encode_pair_group(const uint32_t *set_planes, co
       auto one = [&](auto ic) {
         constexpr int i = decltype(ic)::value;
         if constexpr (r(i) >= 0) {
-#if VDS_ENC_COMBINE_PAAR
+          // P(r) = P0(y) + r P1(y) as one Horner step (its Paar program where
+          // one beats the row form).  Against a multiply and an XOR, same box
+          // (round 4, tools/gpu_ab_trailer.sh): k = 16 encode 13.47 -> 13.31
+          // ms (512 x 64 MiB), k = 32 / n = 40 9.50-9.53 ms either way.
           const Plane16 o0 = plane_horner_enc<(uint32_t)(r(i) >= 0 ? r(i) : 0)>(R1[i], R0[i]);  // R1 r + R0
-#else
-          const Plane16 o0 = plane_xor(R0[i], plane_mulc<(uint32_t)(r(i) >= 0 ? r(i) : 0)>(R1[i]));
-#endif
           store_rep<S::kMap, ST>(o0, rep_ptr(a, r(i)), a, tp, lane, bm);
           store_rep<S::kMap, ST>(plane_xor(o0, R1[i]), rep_ptr(a, r(i) + 1), a, tp, lane, bm);
         }

@@ -329,6 +329,7 @@ struct ParamSlot {
   hipEvent_t copied = nullptr;  // the host -> device copy on the ring's copy stream
   bool pending = false;  // its event guards the device copy's readers
   bool busy = false;     // acquired, not yet released
+  uint64_t stamp = 0;    // when last acquired (ParamRing::clock)
 };
 
 struct ParamRing {
@@ -337,6 +338,7 @@ struct ParamRing {
   std::condition_variable freed;  // a slot was released
   ParamSlot slot[kSlots];
   unsigned next = 0;
+  uint64_t clock = 0;
   hipStream_t copy = nullptr;  // the copies run here, beside the caller's kernels
 };
 
@@ -370,11 +372,16 @@ hipError_t param_acquire_n(int cnt, const size_t *bytes, ParamSlot **out) {
   hipError_t e = hipSuccess;
   if (!r->copy && (e = hipStreamCreateWithFlags(&r->copy, hipStreamNonBlocking)) != hipSuccess) return e;
   // per slot, first choice: an idle slot already big enough whose readers are
-  // done (no allocation, no wait); else the next idle slot in rotation; with
-  // fewer than cnt idle slots, take none and wait for a release.  (Taking a
-  // big slot whose readers are still running instead of growing another made
-  // every call wait for the previous one's kernels: the host planning no
-  // longer overlapped the GPU, live repair 1020 -> 788 GiB/s.)
+  // done (no allocation, no wait); second, once kAhead slots are big enough
+  // but all still being read: the least recently used of them (its event
+  // wait below keeps the caller at most kAhead calls ahead of the GPU); else
+  // the next idle slot in rotation, grown; with fewer than cnt idle slots,
+  // take none and wait for a release.  (Always growing let a caller that
+  // plans faster than the GPU runs grow a new slot on nearly every call of a
+  // loop -- pinned and device allocations, milliseconds each; always waiting
+  // on the one big slot made every call wait for the previous one's kernels,
+  // live repair 1020 -> 788 GiB/s.)
+  constexpr int kAhead = 3;
   ParamSlot *sp[ParamRing::kSlots / 2] = {};
   bool pending[ParamRing::kSlots / 2] = {};
   for (;;) {
@@ -385,12 +392,24 @@ hipError_t param_acquire_n(int cnt, const size_t *bytes, ParamSlot **out) {
         ParamSlot &c = r->slot[(r->next + i) % ParamRing::kSlots];
         if (!c.busy && c.cap >= bytes[got] && (!c.pending || hipEventQuery(c.ev) == hipSuccess)) p = &c;
       }
+      if (!p) {
+        int big = 0;
+        ParamSlot *lru = nullptr;
+        for (int i = 0; i < ParamRing::kSlots; ++i) {
+          ParamSlot &c = r->slot[i];
+          if (c.busy || c.cap < bytes[got]) continue;
+          ++big;
+          if (!lru || c.stamp < lru->stamp) lru = &c;
+        }
+        if (big >= kAhead) p = lru;
+      }
       for (int i = 0; i < ParamRing::kSlots && !p; ++i) {
         ParamSlot &c = r->slot[r->next++ % ParamRing::kSlots];
         if (!c.busy) p = &c;
       }
       if (!p) break;
       p->busy = true;
+      p->stamp = ++r->clock;
       sp[got] = p;
     }
     if (got == cnt) break;

@@ -266,8 +266,8 @@ __global__ void k_regen_tail_batch(uint32_t k, uint32_t m, const SynBatchObj *ob
 //   l_j(t) = prod_{i != j} (t + a_i) / D_j,  D_j = prod_{i != j} (a_j + a_i),
 // the numerator an exclusive product across the lanes (prefix x suffix
 // scans), so the only inversion is D_j's, once per slot.  t equal to a slot's
-// point gives the unit row, as it must.  k <= 32: the wave's two halves take
-// two rows at a time (32-lane scans).
+// point gives the unit row, as it must.  Stored spread (SynBatchRt::coef).
+// k <= 32: the wave's two halves take two rows at a time (32-lane scans).
 __global__ void k_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count) {
   const int lane = threadIdx.x & 63;
   const int seg = k <= 32 ? 32 : 64;  // lanes per row
@@ -288,7 +288,7 @@ __global__ void k_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count) 
       d4[i & 3] = gf16_mul(d4[i & 3], i == (uint32_t)j ? 1u : (a ^ ai));
     }
     const uint32_t invD = gf16_inv_it(gf16_mul(gf16_mul(d4[0], d4[1]), gf16_mul(d4[2], d4[3])));
-    uint16_t *const out = const_cast<uint16_t *>(r.coef);
+    uint32_t *const out = const_cast<uint32_t *>(r.coef);
     for (uint32_t m0 = 0; m0 < ne; m0 += per_pass) {
       const uint32_t m = m0 + (uint32_t)half;
       const uint32_t f = live && m < ne ? (r.epoint[m] ^ a) : 1u;
@@ -300,7 +300,10 @@ __global__ void k_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count) 
       }
       const uint32_t before = __shfl_up(pre, 1), after = __shfl_down(suf, 1);
       const uint32_t excl = gf16_mul(j == 0 ? 1u : before, j == seg - 1 ? 1u : after);
-      if (live && m < ne) out[(uint64_t)m * k + j] = (uint16_t)gf16_mul(excl, invD);
+      if (live && m < ne) {
+        const uint32_t c = gf16_mul(excl, invD);
+        out[(uint64_t)m * k + j] = (c & 0xFFu) | ((c & 0xFF00u) << 8);  // (spread: SynBatchRt::coef)
+      }
     }
   }
 }

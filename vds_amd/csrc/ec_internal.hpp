@@ -164,7 +164,9 @@ constexpr uint32_t kHalfStripes = kTileStripes / 2;
 // rows are Lagrange over the slots' points, computed on the device
 // (launch_rt_coefs) from spoint / epoint.
 struct SynBatchRt {
-  const uint16_t *coef;       // ne x K, row-major, slot order (device)
+  // ne x K, row-major, slot order (device); coefficient c as the spread word
+  // (c & 0xFF) | (c >> 8) << 16, the form the RT walk builds its masks from
+  const uint32_t *coef;
   uint64_t borrowed;          // bit j: slot j holds a survivor beyond K-1
   uint32_t ne;                // rows
   uint32_t pad_;

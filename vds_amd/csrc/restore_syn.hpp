@@ -339,22 +339,48 @@ __device__ __forceinline__ void rec_pair(Plane16 &acc, const Plane16 &t, const P
 // VGPRs, measured no faster than this copy of the mask: 363 vs 377 GiB/s.)
 // The mask is copied to a VGPR first: a v_bitop3 reading an SGPR issues at
 // ~0.6 of the all-VGPR rate.
+//
+// x holds the two halves' coefficients of one (row, slot) as bits 0-7 = half
+// 0's low byte, 8-15 = half 1's, 16-23 / 24-31 the high bytes
+// (SynBatchRt::coef's spread words, half 1's shifted by 8).  Bit b's two bits
+// are then 0x101 << pos(b), and ((x & that) >> pos) * 0x00FF00FF is the
+// plane mask in three SALU, the s_and's SCC (mask nonzero) feeding the
+// branch: against seven (two bit extracts, two selects, an or, a compare)
+// when the mask was built from the two coefficients bit by bit.
 constexpr uint32_t kRtH0 = 0x00FF00FFu, kRtH1 = 0xFF00FF00u;
+// f(IntK<B>{}), .., f(IntK<E - 1>{}) (the run-time compiled kernels include
+// this header under hiprtc, without the standard library's index sequences)
+template <int V> struct IntK {
+  static constexpr int value = V;
+};
+template <int B, int E, class F> __device__ __forceinline__ void static_for(F &&f) {
+  if constexpr (B < E) {
+    f(IntK<B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 #define VDS_RD_MA(i) "v_bitop3_b32 %[c" #i "], %[c" #i "], %[a" #i "], %[tm] bitop3:0x78\n"
 #define VDS_RD_MB(i) "v_bitop3_b32 %[c" #i "], %[c" #i "], %[b" #i "], %[tm] bitop3:0x78\n"
-__device__ __forceinline__ void rec_dual(Plane16 &acc, const Plane16 &t, const Plane16 &t1, uint32_t ma, uint32_t mb) {
-  uint32_t tm;
+template <int BIT>
+__device__ __forceinline__ void rec_dual_x(Plane16 &acc, const Plane16 &t, const Plane16 &t1, uint32_t x) {
+  constexpr uint32_t pa = BIT < 8 ? BIT : BIT + 8, pb = BIT + 1 < 8 ? BIT + 1 : BIT + 9;
+  uint32_t tm, sm;
   asm volatile(
-      "s_cmp_eq_u32 %[ma], 0\n"
-      "s_cbranch_scc1 1f\n"
-      "v_mov_b32 %[tm], %[ma]\n" VDS_RS_SEQ(VDS_RD_MA)
+      "s_and_b32 %[sm], %[x], %[ka]\n"
+      "s_cbranch_scc0 1f\n"
+      "s_lshr_b32 %[sm], %[sm], %[pa]\n"
+      "s_mul_i32 %[sm], %[sm], 0xff00ff\n"
+      "v_mov_b32 %[tm], %[sm]\n" VDS_RS_SEQ(VDS_RD_MA)
       "1:\n"
-      "s_cmp_eq_u32 %[mb], 0\n"
-      "s_cbranch_scc1 2f\n"
-      "v_mov_b32 %[tm], %[mb]\n" VDS_RS_SEQ(VDS_RD_MB)
+      "s_and_b32 %[sm], %[x], %[kb]\n"
+      "s_cbranch_scc0 2f\n"
+      "s_lshr_b32 %[sm], %[sm], %[pb]\n"
+      "s_mul_i32 %[sm], %[sm], 0xff00ff\n"
+      "v_mov_b32 %[tm], %[sm]\n" VDS_RS_SEQ(VDS_RD_MB)
       "2:\n"
-      : VDS_RS_LIST(VDS_RS_C), [tm] "=&v"(tm)
-      : VDS_RS_LIST(VDS_RS_A), VDS_RS_LIST(VDS_RS_B), [ma] "s"(ma), [mb] "s"(mb)
+      : VDS_RS_LIST(VDS_RS_C), [tm] "=&v"(tm), [sm] "=&s"(sm)
+      : VDS_RS_LIST(VDS_RS_A), VDS_RS_LIST(VDS_RS_B), [x] "s"(x), [ka] "i"(0x101u << pa), [kb] "i"(0x101u << pb),
+        [pa] "i"(pa), [pb] "i"(pb)
       : "scc");
 }
 #undef VDS_RD_MA
@@ -808,7 +834,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       const SynBatchObj &d0 = half_obj(tile, 0), &d1 = half_obj(tile, 1);
       rt_rows = s_ld(&a.tiles[tile].nm);
       const uint32_t ne0 = s_ld(&d0.rt.ne), ne1 = s_ld(&d1.rt.ne);
-      const uint16_t *cf0 = s_ld(&d0.rt.coef), *cf1 = s_ld(&d1.rt.coef);
+      const uint32_t *cf0 = s_ld(&d0.rt.coef), *cf1 = s_ld(&d1.rt.coef);
       uint32_t vh0, vh1;  // the half masks in VGPRs (for the scatter)
       asm("v_mov_b32 %0, %1" : "=v"(vh0) : "i"(kRtH0));
       asm("v_mov_b32 %0, %1" : "=v"(vh1) : "i"(kRtH1));
@@ -821,23 +847,20 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
 #pragma unroll
         for (int m = 0; m < kMC; ++m) ce[m] = plane_zero();
         // this wave's kLoadPer = 4 slot coefficients of each row, both
-        // halves: 8 contiguous bytes per (half, row), all issued at once
-        static_assert(S::kLoadPer == 4, "one 8-byte scalar load per row and half");
-        uint64_t q0[kMC], q1[kMC];
+        // halves: 16 contiguous bytes per (half, row), all issued at once
+        static_assert(S::kLoadPer == 4, "one 16-byte scalar load per row and half");
+        u32x4 q0[kMC], q1[kMC];
 #pragma unroll
         for (int m = 0; m < kMC; ++m) {
           const uint32_t at = (m0 + m) * K + wave * S::kLoadPer;
-          q0[m] = m0 + m < ne0 ? s_ld(reinterpret_cast<const uint64_t *>(cf0 + at)) : 0ull;
-          q1[m] = m0 + m < ne1 ? s_ld(reinterpret_cast<const uint64_t *>(cf1 + at)) : 0ull;
+          q0[m] = m0 + m < ne0 ? s_ld(reinterpret_cast<const u32x4 *>(cf0 + at)) : u32x4{0u, 0u, 0u, 0u};
+          q1[m] = m0 + m < ne1 ? s_ld(reinterpret_cast<const u32x4 *>(cf1 + at)) : u32x4{0u, 0u, 0u, 0u};
         }
 #pragma unroll
         for (int s = 0; s < S::kLoadPer; ++s) {
-          uint32_t c0[kMC], c1[kMC];
+          uint32_t x[kMC];  // the (row, slot)'s two coefficients packed for rec_dual_x
 #pragma unroll
-          for (int m = 0; m < kMC; ++m) {
-            c0[m] = (uint32_t)(q0[m] >> (16 * s)) & 0xFFFFu;
-            c1[m] = (uint32_t)(q1[m] >> (16 * s)) & 0xFFFFu;
-          }
+          for (int m = 0; m < kMC; ++m) x[m] = q0[m][s] | (q1[m][s] << 8);
           // (one slot's chain at a time: interleaving the four independent
           // chains would not fit beside the accumulators)
           __builtin_amdgcn_sched_barrier(0);
@@ -846,18 +869,14 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
           // out of the loop all 4 x 16 of them spilled)
 #pragma unroll
           for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(tt.p[i]));
-#pragma unroll
-          for (int b = 0; b < 16; b += 2) {
+          static_for<0, 8>([&](auto bp) {
+            constexpr int b = 2 * decltype(bp)::value;
             __builtin_amdgcn_sched_barrier(0);
             const Plane16 t1 = plane_mulx(tt);
 #pragma unroll
-            for (int m = 0; m < kMC; ++m) {
-              const uint32_t ma = (((c0[m] >> b) & 1u) ? kRtH0 : 0u) | (((c1[m] >> b) & 1u) ? kRtH1 : 0u);
-              const uint32_t mb = (((c0[m] >> (b + 1)) & 1u) ? kRtH0 : 0u) | (((c1[m] >> (b + 1)) & 1u) ? kRtH1 : 0u);
-              rec_dual(ce[m], tt, t1, ma, mb);
-            }
-            if (b < 14) tt = plane_mulx(t1);
-          }
+            for (int m = 0; m < kMC; ++m) rec_dual_x<b>(ce[m], tt, t1, x[m]);
+            if constexpr (b < 14) tt = plane_mulx(t1);
+          });
         }
 #pragma unroll
         for (int m = 0; m < kMC; ++m) {

@@ -38,6 +38,14 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) { return __buil
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
+// Ch(e, f, g) = e ? f : g and Maj(a, b, c) as one v_bitop3_b32 each (0xCA, 0xE8);
+// left to the compiler they came out as two to three ops per round.
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
 
 // One compression of the 16 big-endian message words w (w is the schedule ring).
 __device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[16]) {
@@ -50,8 +58,8 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[
       const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
       w[i & 15] += s0 + w[(i + 9) & 15] + s1;
     }
-    const uint32_t t1 = hh + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ((e & f) ^ (~e & g)) + kSha256K[i] + w[i & 15];
-    const uint32_t t2 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    const uint32_t t1 = hh + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ch(e, f, g) + kSha256K[i] + w[i & 15];
+    const uint32_t t2 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c);
     hh = g;
     g = f;
     f = e;

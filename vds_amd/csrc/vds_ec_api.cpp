@@ -1753,7 +1753,7 @@ struct RtBatchBuild {
     cap_rows = rows;
     o_tiles = up16(((size_t)count + 1) * sizeof(SynBatchObj));
     o_coef = up16(o_tiles + cap_tiles * sizeof(SynBatchTile));
-    return o_coef + cap_rows * k * sizeof(uint16_t) + 16;
+    return o_coef + cap_rows * k * sizeof(uint32_t) + 16;
   }
   void attach(ParamSlot *sl) {
     slot = sl;
@@ -1791,7 +1791,7 @@ struct RtBatchBuild {
     d.rt.borrowed = borrowed;
     d.rt.ne = ne;
     for (uint32_t m = 0; m < ne; ++m) d.rt.epoint[m] = rowp[m];
-    d.rt.coef = reinterpret_cast<const uint16_t *>(slot->d + o_coef + row0 * k * sizeof(uint16_t));
+    d.rt.coef = reinterpret_cast<const uint32_t *>(slot->d + o_coef + row0 * k * sizeof(uint32_t));
     d.plan = 0;
     obj_halves[i] = halves;
     return d;

@@ -18,6 +18,9 @@ python tools/pmc_traffic.py $D/pmc_fetch32 $D/pmc_write32 32 $D/traffic_k32.json
 echo "[6/8] sq/lds k16"; timeout -k 10 240 $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY -d $D/pmc_sq -o run -- python tools/prof_kernels.py --objects 64 --iters 2 > $D/pmc_sq.log 2>&1 &&
 timeout -k 10 240 $P --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d $D/pmc_lds -o run -- python tools/prof_kernels.py --objects 64 --iters 2 > $D/pmc_lds.log 2>&1 &&
 echo "[7/8] live trace"; timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $D/live -o run -- python tools/live_prof.py --objects 16384 --loss 0.02 0.25 --steps 10 > $D/live_prof.log 2>&1 &&
+echo "[7b] live sq"; timeout -k 10 300 $P --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d $D/pmc_live_sq -o run -- python tools/live_prof.py --objects 16384 --loss 0.02 0.25 --steps 3 > $D/pmc_live_sq.log 2>&1 &&
+timeout -k 10 300 $P --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE -d $D/pmc_live_sq2 -o run -- python tools/live_prof.py --objects 16384 --loss 0.02 0.25 --steps 3 > $D/pmc_live_sq2.log 2>&1 &&
+python tools/pmc_kernels.py $D/pmc_live_kernels.json $D/pmc_live_sq $D/pmc_live_sq2 > $D/pmc_live_kernels.txt &&
 echo "[8/8] host"; timeout -k 10 400 python tools/bench_host.py --objects 16 --live 16384 > $D/bench_host.log 2>&1
 rc=$?
 echo "rc=$rc"

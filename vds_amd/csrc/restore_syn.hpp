@@ -669,7 +669,11 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       }
       if constexpr (kScatter) {  // the fill shares meet in these slots (LDS XOR atomics)
         if (wave < FillP::kFill) {
-          const u32x4 z = {0u, 0u, 0u, 0u};
+          // (zeros made here, per tile: left to the compiler, the zero vector
+          // lived across the loop and was the run-time kernels' 16-byte spill)
+          uint32_t zr;
+          asm volatile("v_mov_b32 %0, 0" : "=v"(zr));
+          const u32x4 z = {zr, zr, zr, zr};
 #pragma unroll
           for (int g = 0; g < 4; ++g) L.put(4 * (int)FillP::kPoint[wave < FillP::kFill ? wave : 0] + g, z);
         }

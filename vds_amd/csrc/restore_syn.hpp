@@ -669,11 +669,12 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       }
       if constexpr (kScatter) {  // the fill shares meet in these slots (LDS XOR atomics)
         if (wave < FillP::kFill) {
-          // (zeros made here, per tile: left to the compiler, the zero vector
-          // lived across the loop and was the run-time kernels' 16-byte spill)
-          uint32_t zr;
-          asm volatile("v_mov_b32 %0, 0" : "=v"(zr));
-          const u32x4 z = {zr, zr, zr, zr};
+          // (this zero vector lives across the tile loop and is the run-time
+          // kernels' 16-byte scratch spill, reloaded once per tile; made per
+          // tile instead -- Scratch_Size 0 -- the k = 16 repair measured ~1%
+          // slower: 14.40-14.65 vs 14.33-14.36 ms, 512 x 64 MiB, three
+          // interleaved rounds, profiles/round4/ablog/zero_spill_ab.log)
+          const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
           for (int g = 0; g < 4; ++g) L.put(4 * (int)FillP::kPoint[wave < FillP::kFill ? wave : 0] + g, z);
         }

@@ -3,9 +3,10 @@
 
   python tools/pmc_kernels.py OUT.json DIR [DIR ...]
 
-Kernel names are cut at the first "(" (the template argument list is
-kept: k_restore_syn instantiations differ only there).  Also printed as a
-table: kernel, dispatches, counters."""
+Kernels are keyed by name and Kernel_Id: with rocprofv3 -T the names are
+truncated, and the instantiations of one template (k_restore_syn's MULTI,
+RT, regenerate ...) differ only in the id (match ids to full names with an
+untruncated --kernel-trace of the same command).  Also printed as a table."""
 import csv
 import glob
 import json
@@ -25,7 +26,8 @@ def main():
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                key = f'{short(r["Kernel_Name"])} id={r["Kernel_Id"]} vgpr={r["VGPR_Count"]} sgpr={r["SGPR_Count"]}'
+                acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     res = {}
     for kn, cs in acc.items():
         res[kn] = {"dispatches": max(len(v) for v in cs.values()),

@@ -308,3 +308,44 @@ def test_regenerate_batch_perm_noncodeword(gpu, k):
         g = os_[0].cpu().numpy()
         assert np.array_equal(g[:L], ws[0]), (i, L, targets[i])
         assert (g[L:] == 0x5A).all()
+
+
+def test_restore_batch_rt2_rows_noncodeword(gpu):
+    """RT2 (k = 32, every survivor below 2k, at most 8 erased points below k:
+    the PERM evaluations of P0 and the |E| x |E| products, ec_internal.hpp)
+    beside RT (9+ rows) in one batch call: random survivors, every trailer
+    kind, 1..12 rows, objects of one to three tiles and tiles whose halves
+    have different row counts, borrowed ids in any order."""
+    import torch
+    from vds_amd import chunk
+    k = 32
+    rng = np.random.default_rng(4242)
+    Ts = [1, 7, 1023, 1024, 1025, 2048, 3000, 5000]
+    pvals = [0, 1, 2 * k - 1, 2 * k - 2, 2 * k, 5]
+    nodes, keep, chunks, csz, pads, outs, want = [], [], [], [], [], [], []
+    for i in range(72):
+        T = Ts[i % len(Ts)]
+        p = pvals[i % len(pvals)]
+        if p == 2 * k and T == 1:
+            p = 0
+        rows = 1 + (i * 7) % 12
+        erased = set(rng.choice(k, rows, replace=False).tolist())
+        nd = [a for a in range(k) if a not in erased] + sorted(rng.choice(np.arange(k, 2 * k), rows, replace=False).tolist())
+        if i % 3 == 1:
+            nd = list(rng.permutation(nd))
+        sv = _survivors(rng, k, T, p, vary=(i % 5 == 0))
+        bufs = [torch.from_numpy(b).cuda() for b in sv]
+        keep.append(bufs)
+        nodes.append(nd)
+        chunks.append([b.data_ptr() for b in bufs])
+        csz.append(2 * T + 2)
+        pads.append(p)
+        w = O.restore(k, nd, sv)
+        want.append(w)
+        outs.append(torch.full((w.size + 64,), 0xA5, dtype=torch.uint8, device="cuda"))
+    chunk.restore_batch_device(k, nodes, chunks, csz, pads, [o.data_ptr() for o in outs])
+    torch.cuda.synchronize()
+    for i, (w, o) in enumerate(zip(want, outs)):
+        g = o.cpu().numpy()
+        assert np.array_equal(g[:w.size], w), (i, csz[i], pads[i], nodes[i])
+        assert (g[w.size:] == 0xA5).all()

@@ -279,6 +279,35 @@ __global__ void k_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count) 
     const SynBatchRt &r = objs[o].rt;
     const uint32_t ne = r.ne;
     if (ne == 0) continue;
+    if (r.mode == 1) {  // RT2 rows (SynBatchRt, ec_internal.hpp): c[m][jj] = F_m G_jj / (e_m + b_jj)
+      uint32_t *const out = const_cast<uint32_t *>(r.coef);
+      const uint64_t erased = r.borrowed;  // (the erased points below k: the borrowed slots)
+      // lanes 0..ne-1: x = e_m; lanes 16..16+ne-1: x = b_jj; Z(x) over the survivors below k
+      const int q = lane & 15;
+      const bool isb = lane >= 16 && lane < 32;
+      const uint32_t em = q < (int)ne ? r.epoint[q] : 0u;
+      const uint32_t x = q < (int)ne ? (isb ? r.spoint[em] : em) : 0u;
+      uint32_t z = 1u;
+      for (uint32_t a = 0; a < k; ++a) z = gf16_mul(z, ((erased >> a) & 1u) ? 1u : (x ^ a));
+      // F_m = Z(e_m) prod_i (e_m + b_i); G_jj = 1 / (Z(b_jj) prod_{i != jj} (b_jj + b_i))
+      uint32_t fg = z;
+      for (uint32_t i = 0; i < ne; ++i) {
+        const uint32_t bi = __shfl(x, 16 + (int)i);
+        fg = gf16_mul(fg, (isb && (uint32_t)q == i) ? 1u : (x ^ bi));
+      }
+      if (isb) fg = gf16_inv_it(fg);
+      for (uint32_t pr = (uint32_t)lane; pr < 64u * ((ne * ne + 63) / 64); pr += 64) {
+        const uint32_t m = pr / ne, jj = pr % ne;
+        const bool ok = pr < ne * ne;
+        const uint32_t F = __shfl(fg, ok ? (int)m : 0), G = __shfl(fg, ok ? 16 + (int)jj : 16);
+        const uint32_t e = __shfl(x, ok ? (int)m : 0), b = __shfl(x, ok ? 16 + (int)jj : 16);
+        if (ok) {
+          const uint32_t c = gf16_mul(gf16_mul(F, G), gf16_inv_it(e ^ b));
+          out[(uint64_t)m * k + jj] = (c & 0xFFu) | ((c & 0xFF00u) << 8);
+        }
+      }
+      continue;
+    }
     const bool live = j < (int)k;
     const uint32_t a = live ? r.spoint[j] : 0u;
     // D_j in four independent chains (ILP)

@@ -169,10 +169,20 @@ struct SynBatchRt {
   const uint32_t *coef;
   uint64_t borrowed;          // bit j: slot j holds a survivor beyond K-1
   uint32_t ne;                // rows
-  uint32_t pad_;
+  uint32_t mode;              // restore, k = 32: 1 = RT2 rows (kRt2MaxRows, below), else 0
   uint8_t epoint[kMaxFastK];  // point of output row m
   uint8_t spoint[kMaxFastK];  // point held by slot j
 };
+// RT2 (restore, k = 32, every survivor below 2k, at most kRt2MaxRows erased
+// points below k): with A the survivors below k, E the erased points and b_j
+// the survivor borrowed into slot e_j, P = P0 + Z Q where P0 interpolates the
+// values on U = {0..k-1} with zeros at E (so P0(b) is the PERM program's
+// permuted sum), Z = prod_{a in A} (X + a) and deg Q < |E|.  Then
+//   P(e_m) = sum_j c[m][j] r_j,  r_j = y_(b_j) + P0(b_j),
+//   c[m][j] = Z(e_m) prod_{i != j} (e_m + b_i) / (Z(b_j) prod_{i != j} (b_j + b_i)):
+// |E| fixed PERM evaluations and |E|^2 runtime products instead of RT's
+// |E| k.  coef holds c (row m, column j < ne) in RT's spread form.
+constexpr uint32_t kRt2MaxRows = 8;  // (one r_j per free LDS slot K..K+7 of the k = 32 kernel)
 struct SynBatchObj {
   const uint8_t *chunks[kMaxFastK];  // survivor j = the chunk of plan point j (K used); RT: of slot j
   uint8_t *out;                      // restore: the object's bytes
@@ -206,7 +216,7 @@ struct SynBatchTile {
   uint32_t plan;        // (RT: unused)
   uint32_t trailer;     // regenerate: bit h = half h also copies its object's trailer cell
   uint32_t nm;          // RT: rows of the tile = max ne over its halves
-  uint32_t pad_;
+  uint32_t mode;        // RT: SynBatchRt::mode of both halves (the host never pairs two modes)
 };
 
 // Reference-route tail of a regenerate.  The reference repairs a replica by

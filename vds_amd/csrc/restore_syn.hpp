@@ -659,8 +659,13 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     const bool perm_tile = kPerm || (kMulti && REGEN && cls == kClsPerm);
     const int my_erased = RT ? K + wave : perm_tile ? K : (wave < S::kM ? erased_of(wave) : 0);
     Plane16 Ps[RT ? S::kLoadPer : 1];  // RT: this wave's slots, kept for phase 2
+    // RT2 tile (SynBatchRt, ec_internal.hpp): restore at k = 32 through the
+    // PERM evaluations of P0 and |E| x |E| runtime products
+    constexpr bool kRt2 = RT && !REGEN && K == 32 && N >= K + 8;
+    const bool rt2_tile = kRt2 && s_ld(&a.tiles[tile].mode) == 1u;
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
     syn_prio<1, kPrio>();
+    uint64_t bor[2] = {0, 0};  // RT restore: borrowed slots of each half
     {
       if (wave < S::kM && (!RT || REGEN) && !FILL && (!perm_tile || wave == 0)) {
         const u32x4 z = {0u, 0u, 0u, 0u};
@@ -679,7 +684,11 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
           for (int g = 0; g < 4; ++g) L.put(4 * (int)FillP::kPoint[wave < FillP::kFill ? wave : 0] + g, z);
         }
       }
-      uint64_t bor[2] = {0, 0};  // RT restore: borrowed slots of each half
+      if (rt2_tile) {  // RT2: slot K + wave collects r_j of row j = wave in phase 2
+        const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) L.put(4 * (K + wave) + g, z);
+      }
       if constexpr (RT && !REGEN) {
         bor[0] = s_ld(&half_obj(tile, 0).rt.borrowed);
         bor[1] = s_ld(&half_obj(tile, 1).rt.borrowed);
@@ -846,6 +855,90 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       // two rows per walk of each slot's chain, the pairs in a rolled loop
       // (code size: see rec_dual)
       constexpr int kMC = 2;
+      if (rt2_tile) {
+        if constexpr (kRt2) {
+          // ---- 2 (RT2, at most 8 rows: slots K..K+7 collect r_j). (a) this
+          // wave's borrowed survivors y_(b_j) into slot K + j (their half's
+          // bits), (b) the PERM program's P0(b_j) of both halves (reads through
+          // c -> c ^ t'_h, merged by half) into the same slots, barrier, (c)
+          // row m = wave: sum_j c[m][j] r_j by the x^b chains of the r_j, (d)
+          // P(e_m) into the erased slots (zero in their halves until now)
+          const uint8_t *ep0 = d0.rt.epoint, *ep1 = d1.rt.epoint, *sp0 = d0.rt.spoint, *sp1 = d1.rt.spoint;
+          // (a)
+#pragma unroll
+          for (int sl = 0; sl < S::kLoadPer; ++sl) {
+            const int slot = wave * S::kLoadPer + sl;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+              if ((bor[h] >> slot) & 1u) {
+                const int j = __builtin_popcountll(bor[h] & ((1ull << slot) - 1));
+                Plane16 v;
+#pragma unroll
+                for (int b = 0; b < 16; ++b) v.p[b] = Ps[sl].p[b] & (h ? vh1 : vh0);
+                lds_xor_point(L, K + j, v);
+              }
+          }
+          // (b)
+#pragma clang loop unroll(disable)
+          for (uint32_t j = 0; j < rt_rows; ++j) {
+            const bool h0 = j < ne0, h1 = j < ne1;
+            const uint32_t t0 = h0 ? s_ld_u8(sp0, (int)s_ld_u8(ep0, (int)j)) - (uint32_t)K : 0u;
+            const uint32_t t1 = h1 ? s_ld_u8(sp1, (int)s_ld_u8(ep1, (int)j)) - (uint32_t)K : 0u;
+            struct Rt2In {
+              const SynLds &L;
+              uint32_t t0, t1, m0, m1;
+              __device__ __forceinline__ u32x4 operator()(int g) const {
+                const u32x4 x0 = L(4 * (int)((uint32_t)(g >> 2) ^ t0) + (g & 3));
+                const u32x4 x1 = L(4 * (int)((uint32_t)(g >> 2) ^ t1) + (g & 3));
+                return (x0 & m0) | (x1 & m1);
+              }
+            } in{L, t0, t1, h0 ? vh0 : 0u, h1 ? vh1 : 0u};
+            uint32_t pacc[16];
+            PermSyn<K>::part(wave, in, pacc);
+            lds_xor_point(L, K + (int)j, *reinterpret_cast<const Plane16 *>(pacc));
+          }
+          __syncthreads();  // the r_j are whole
+          if ((uint32_t)wave < rt_rows) {
+            // (c)
+            const uint32_t m = (uint32_t)wave;
+            Plane16 racc = plane_zero();
+#pragma clang loop unroll(disable)
+            for (uint32_t j = 0; j < rt_rows; ++j) {
+              const uint32_t c0 = (m < ne0 && j < ne0) ? s_ld(cf0 + (m * K + j)) : 0u;
+              const uint32_t c1 = (m < ne1 && j < ne1) ? s_ld(cf1 + (m * K + j)) : 0u;
+              const uint32_t x = c0 | (c1 << 8);
+              Plane16 tt;
+              syn_get_point(L, K + (int)j, tt.p);
+              static_for<0, 8>([&](auto bp) {
+                constexpr int b = 2 * decltype(bp)::value;
+                __builtin_amdgcn_sched_barrier(0);
+                const Plane16 t1 = plane_mulx(tt);
+                rec_dual_x<b>(racc, tt, t1, x);
+                if constexpr (b < 14) tt = plane_mulx(t1);
+              });
+            }
+            // (d)
+            const int p0 = m < ne0 ? (int)s_ld_u8(ep0, (int)m) : -1;
+            const int p1 = m < ne1 ? (int)s_ld_u8(ep1, (int)m) : -1;
+            if (p0 >= 0 && p0 == p1) {
+              lds_xor_point(L, p0, racc);
+            } else {
+              if (p0 >= 0) {
+                Plane16 v;
+#pragma unroll
+                for (int b = 0; b < 16; ++b) v.p[b] = racc.p[b] & vh0;
+                lds_xor_point(L, p0, v);
+              }
+              if (p1 >= 0) {
+                Plane16 v;
+#pragma unroll
+                for (int b = 0; b < 16; ++b) v.p[b] = racc.p[b] & vh1;
+                lds_xor_point(L, p1, v);
+              }
+            }
+          }
+        }
+      } else
 #pragma clang loop unroll(disable)
       for (uint32_t m0 = 0; m0 < rt_rows; m0 += kMC) {
         Plane16 ce[kMC];

@@ -1734,8 +1734,19 @@ struct SynBatchBuild {
 // halves are paired in order of row count.  One pinned slot holds the
 // objects, the tiles and -- device side only, written by the coefficient
 // kernel -- the rows.  fill() may run on several threads for distinct i.
+// RT2 rows for the k = 32 restore's RT objects (VDS_EC_RT2=0: every RT
+// object takes the k-slot combination, A/B)
+bool rt2_enabled() {
+  static const bool on = [] {
+    const char *v = std::getenv("VDS_EC_RT2");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 struct RtBatchBuild {
   uint32_t k, n;
+  bool rt2 = false;  // restore: objects that qualify take RT2 rows (SynBatchRt::mode)
   ParamSlot *slot = nullptr;
   size_t cap_tiles = 0, o_tiles = 0, o_coef = 0;
   uint64_t cap_rows = 0;
@@ -1790,6 +1801,12 @@ struct RtBatchBuild {
     }
     d.rt.borrowed = borrowed;
     d.rt.ne = ne;
+    // RT2 (ec_internal.hpp): k = 32, 1..kRt2MaxRows rows, every borrowed
+    // survivor in k..2k-1 (the PERM program's coset)
+    bool two = rt2 && k == 32 && ne >= 1 && ne <= kRt2MaxRows;
+    for (uint32_t a = 0; two && a < k; ++a)
+      if (((borrowed >> a) & 1u) && d.rt.spoint[a] >= 2 * k) two = false;
+    d.rt.mode = two ? 1u : 0u;
     for (uint32_t m = 0; m < ne; ++m) d.rt.epoint[m] = rowp[m];
     d.rt.coef = reinterpret_cast<const uint32_t *>(slot->d + o_coef + row0 * k * sizeof(uint32_t));
     d.plan = 0;
@@ -1800,29 +1817,35 @@ struct RtBatchBuild {
     if (nobj == 0) return hip_status(param_release(slot, s));
     const uint32_t empty = nobj;
     std::memset(&objs[empty], 0, sizeof(SynBatchObj));
-    // objects by row count (counting sort), halves paired in that order
-    std::vector<uint32_t> cnt(kMaxFastK + 2, 0), order(nobj);
-    for (uint32_t o = 0; o < nobj; ++o) ++cnt[objs[o].rt.ne + 1];
+    // objects by (mode, row count) (counting sort: RT2 objects first), halves
+    // paired in that order; a tile never pairs the two modes (the kernel's
+    // phase 2 is per tile)
+    const uint32_t kKeys = kMaxFastK + 1;
+    std::vector<uint32_t> cnt(2 * kKeys + 1, 0), order(nobj);
+    auto key = [&](uint32_t o) { return (objs[o].rt.mode == 1u ? 0u : kKeys) + objs[o].rt.ne; };
+    for (uint32_t o = 0; o < nobj; ++o) ++cnt[key(o) + 1];
     for (uint32_t r = 1; r < cnt.size(); ++r) cnt[r] += cnt[r - 1];
-    for (uint32_t o = 0; o < nobj; ++o) order[cnt[objs[o].rt.ne]++] = o;
+    for (uint32_t o = 0; o < nobj; ++o) order[cnt[key(o)]++] = o;
     uint64_t total = 0;
     for (uint32_t o = 0; o < nobj; ++o) total += obj_halves[o];
-    const uint64_t ntiles = (total + 1) / 2;
-    if (ntiles > cap_tiles || ntiles > 0xFFFFFFFFull) {
+    if ((total + 2) / 2 > cap_tiles || (total + 2) / 2 > 0xFFFFFFFFull) {  // (+1 half: the mode boundary)
       (void)param_release(slot, s);
       return VDS_EC_EINVAL;
     }
     SynBatchTile *tiles = reinterpret_cast<SynBatchTile *>(slot->h + o_tiles);
     uint64_t i = 0;
-    for (const uint32_t o : order)
+    for (const uint32_t o : order) {
+      if ((i & 1) && tiles[i / 2].mode != objs[o].rt.mode) ++i;  // (the other mode starts a new tile)
       for (uint32_t h = 0; h < obj_halves[o]; ++h, ++i) {
         SynBatchTile &t = tiles[i / 2];
-        if ((i & 1) == 0) t = SynBatchTile{{empty, empty}, {0, 0}, 0, 0, 0, 0};
+        if ((i & 1) == 0) t = SynBatchTile{{empty, empty}, {0, 0}, 0, 0, 0, objs[o].rt.mode};
         t.obj[i & 1] = o;
         t.stripe0[i & 1] = h * kHalfStripes;
         t.nm = std::max(t.nm, objs[o].rt.ne);
         if (regen && h + 1 == obj_halves[o]) t.trailer |= 1u << (i & 1);
       }
+    }
+    const uint64_t ntiles = (i + 1) / 2;
     hipError_t e = param_commit(slot, o_tiles + ntiles * sizeof(SynBatchTile), s);
     const SynBatchObj *dobjs = reinterpret_cast<const SynBatchObj *>(slot->d);
     if (e == hipSuccess) e = launch_rt_coefs(k, dobjs, nobj, s);
@@ -2016,6 +2039,7 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
   ix.build(info);
   SynBatchBuild bb{k, n};
   RtBatchBuild rb{k, n};
+  rb.rt2 = rt2_enabled();  // (restore only; RtBatchBuild::fill decides per object)
   std::vector<uint32_t> plan;
   ht.mark("index");
   if ((rc = batch_begin(info, ix, bb, rb, plan, s))) return rc;

@@ -6,6 +6,8 @@
 // those are not instantiated for (e.g. chunk_storage's 800-of-1000 ids, the
 // uint8_t template, the cell-array test paths).  Plus the synthetic-object
 // generator used by bench.py and the tests.
+#include <mutex>
+
 #include "ec_device.hpp"
 
 namespace vds_ec {
@@ -260,14 +262,48 @@ __global__ void k_regen_tail_batch(uint32_t k, uint32_t m, const SynBatchObj *ob
   }
 }
 
+// GF(2^16) log / exp tables (generator x = 2 of kPoly16, as the reference's
+// gf_math<uint16_t>, gf.h:193-253): the RT coefficient kernel's products
+// become sums of logs.  g_exp16 is 3 x 65535 long so a sum of three reduced
+// logs needs no reduction.  Built once per device by k_gf16_tables.
+__device__ uint16_t g_log16[65536];
+__device__ uint16_t g_exp16[3 * 65535];
+
+__global__ void k_gf16_tables() {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 65535) return;
+  uint32_t r = 1, b = 2, e = i;  // 2^i
+  while (e) {
+    if (e & 1u) r = gf16_mul(r, b);
+    b = gf16_mul(b, b);
+    e >>= 1;
+  }
+  g_exp16[i] = g_exp16[i + 65535] = g_exp16[i + 2 * 65535] = (uint16_t)r;
+  g_log16[r] = (uint16_t)i;
+  if (i == 0) g_log16[0] = 0;  // (never read: zero factors are handled apart)
+}
+
+__device__ __forceinline__ uint32_t glog(uint32_t x) { return g_log16[x]; }
+__device__ __forceinline__ uint32_t mod65535(uint32_t x) {
+  x = (x & 0xFFFFu) + (x >> 16);
+  x = (x & 0xFFFFu) + (x >> 16);
+  return x >= 65535u ? x - 65535u : x;
+}
+__device__ __forceinline__ uint32_t spread16(uint32_t c) { return (c & 0xFFu) | ((c & 0xFF00u) << 8); }
+
 // RT coefficient rows (SynBatchRt): one wave per object, lane j = slot j
 // holding point a_j.  Row m, column j is the Lagrange basis polynomial of
 // slot j evaluated at t = epoint[m]:
-//   l_j(t) = prod_{i != j} (t + a_i) / D_j,  D_j = prod_{i != j} (a_j + a_i),
-// the numerator an exclusive product across the lanes (prefix x suffix
-// scans), so the only inversion is D_j's, once per slot.  t equal to a slot's
-// point gives the unit row, as it must.  Stored spread (SynBatchRt::coef).
-// k <= 32: the wave's two halves take two rows at a time (32-lane scans).
+//   l_j(t) = prod_i (t + a_i) / ((t + a_j) D_j),  D_j = prod_{i != j} (a_j + a_i),
+// in logs: the row's sum over the lanes (butterfly), minus the lane's two
+// logs, one exp lookup.  t equal to a slot's point gives the unit row.  k <=
+// 32: the wave's two halves take two rows at a time (32-lane segments).
+// (Round 3 multiplied with the carry-less gf16_mul -- ~70 VALU each, prefix
+// and suffix scans per row: 190-200 us per live p = 0.25 call.)
+// RT2 objects (SynBatchRt::mode 1, ec_internal.hpp): c[m][jj] = F_m G_jj /
+// (e_m + b_jj), F_m = Z(e_m) prod_i (e_m + b_i), G_jj = 1 / (Z(b_jj)
+// prod_{i != jj} (b_jj + b_i)), Z(x) = prod over the survivors below k.
+// Stored spread (SynBatchRt::coef).
 __global__ void k_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count) {
   const int lane = threadIdx.x & 63;
   const int seg = k <= 32 ? 32 : 64;  // lanes per row
@@ -279,62 +315,79 @@ __global__ void k_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count) 
     const SynBatchRt &r = objs[o].rt;
     const uint32_t ne = r.ne;
     if (ne == 0) continue;
-    if (r.mode == 1) {  // RT2 rows (SynBatchRt, ec_internal.hpp): c[m][jj] = F_m G_jj / (e_m + b_jj)
-      uint32_t *const out = const_cast<uint32_t *>(r.coef);
+    uint32_t *const out = const_cast<uint32_t *>(r.coef);
+    if (r.mode == 1) {
       const uint64_t erased = r.borrowed;  // (the erased points below k: the borrowed slots)
-      // lanes 0..ne-1: x = e_m; lanes 16..16+ne-1: x = b_jj; Z(x) over the survivors below k
+      // lanes 0..ne-1: x = e_m; lanes 16..16+ne-1: x = b_jj; log Z(x) over the survivors below k
       const int q = lane & 15;
       const bool isb = lane >= 16 && lane < 32;
       const uint32_t em = q < (int)ne ? r.epoint[q] : 0u;
       const uint32_t x = q < (int)ne ? (isb ? r.spoint[em] : em) : 0u;
-      uint32_t z = 1u;
-      for (uint32_t a = 0; a < k; ++a) z = gf16_mul(z, ((erased >> a) & 1u) ? 1u : (x ^ a));
-      // F_m = Z(e_m) prod_i (e_m + b_i); G_jj = 1 / (Z(b_jj) prod_{i != jj} (b_jj + b_i))
-      uint32_t fg = z;
+      uint32_t lz = 0;
+      for (uint32_t a = 0; a < k; ++a)
+        if (!((erased >> a) & 1u)) lz += glog(x ^ a);
+      // log F_m (lanes 0..15), log of 1 / G_jj (lanes 16..31)
       for (uint32_t i = 0; i < ne; ++i) {
         const uint32_t bi = __shfl(x, 16 + (int)i);
-        fg = gf16_mul(fg, (isb && (uint32_t)q == i) ? 1u : (x ^ bi));
+        if (!(isb && (uint32_t)q == i)) lz += glog(x ^ bi);
       }
-      if (isb) fg = gf16_inv_it(fg);
+      const uint32_t lfg = mod65535(lz);
       for (uint32_t pr = (uint32_t)lane; pr < 64u * ((ne * ne + 63) / 64); pr += 64) {
         const uint32_t m = pr / ne, jj = pr % ne;
         const bool ok = pr < ne * ne;
-        const uint32_t F = __shfl(fg, ok ? (int)m : 0), G = __shfl(fg, ok ? 16 + (int)jj : 16);
+        const uint32_t lF = __shfl(lfg, ok ? (int)m : 0), lG = __shfl(lfg, ok ? 16 + (int)jj : 16);
         const uint32_t e = __shfl(x, ok ? (int)m : 0), b = __shfl(x, ok ? 16 + (int)jj : 16);
-        if (ok) {
-          const uint32_t c = gf16_mul(gf16_mul(F, G), gf16_inv_it(e ^ b));
-          out[(uint64_t)m * k + jj] = (c & 0xFFu) | ((c & 0xFF00u) << 8);
+        if (ok) {  // F G / (e + b): lF - lG - log(e + b), shifted positive
+          const uint32_t c = g_exp16[lF + (65535u - lG) + (65535u - glog(e ^ b))];
+          out[(uint64_t)m * k + jj] = spread16(c);
         }
       }
       continue;
     }
     const bool live = j < (int)k;
     const uint32_t a = live ? r.spoint[j] : 0u;
-    // D_j in four independent chains (ILP)
-    uint32_t d4[4] = {1u, 1u, 1u, 1u};
+    // log D_j
+    uint32_t ld = 0;
     for (uint32_t i = 0; i < k; ++i) {
       const uint32_t ai = __shfl(a, (int)i);
-      d4[i & 3] = gf16_mul(d4[i & 3], i == (uint32_t)j ? 1u : (a ^ ai));
+      if (i != (uint32_t)j) ld += glog(a ^ ai);
     }
-    const uint32_t invD = gf16_inv_it(gf16_mul(gf16_mul(d4[0], d4[1]), gf16_mul(d4[2], d4[3])));
-    uint32_t *const out = const_cast<uint32_t *>(r.coef);
+    const uint32_t nld = 65535u - mod65535(ld);  // log of 1 / D_j
     for (uint32_t m0 = 0; m0 < ne; m0 += per_pass) {
       const uint32_t m = m0 + (uint32_t)half;
-      const uint32_t f = live && m < ne ? (r.epoint[m] ^ a) : 1u;
-      uint32_t pre = f, suf = f;  // inclusive prefix / suffix products within the row's lanes
-      for (int off = 1; off < seg; off <<= 1) {
-        const uint32_t u = __shfl_up(pre, off), w = __shfl_down(suf, off);
-        if (j >= off) pre = gf16_mul(pre, u);
-        if (j + off < seg) suf = gf16_mul(suf, w);
-      }
-      const uint32_t before = __shfl_up(pre, 1), after = __shfl_down(suf, 1);
-      const uint32_t excl = gf16_mul(j == 0 ? 1u : before, j == seg - 1 ? 1u : after);
+      const uint32_t f = live && m < ne ? (r.epoint[m] ^ a) : 1u;  // (dead lanes: log 1 = 0)
+      const bool zero = f == 0u;                                   // t is this slot's point
+      const uint64_t zb = __ballot(zero);
+      const bool row_zero = ((zb >> (half * seg)) & (seg == 64 ? ~0ull : 0xFFFFFFFFull)) != 0;
+      uint32_t lf = zero ? 0u : glog(f);
+      uint32_t sum = lf;
+      for (int off = 1; off < seg; off <<= 1) sum += __shfl_xor(sum, off);
       if (live && m < ne) {
-        const uint32_t c = gf16_mul(excl, invD);
-        out[(uint64_t)m * k + j] = (c & 0xFFu) | ((c & 0xFF00u) << 8);  // (spread: SynBatchRt::coef)
+        uint32_t c;
+        if (row_zero)
+          c = zero ? 1u : 0u;
+        else  // prod_i f_i / f_j / D_j
+          c = g_exp16[mod65535(sum) + (65535u - lf) + nld];
+        out[(uint64_t)m * k + j] = spread16(c);
       }
     }
   }
+}
+
+static std::mutex g_tables_mu;
+static uint64_t g_tables_ready = 0;  // bit d: device d has the log / exp tables (g_tables_mu)
+
+static hipError_t ensure_gf16_tables(hipStream_t s) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(g_tables_mu);
+  if (dev < 64 && ((g_tables_ready >> dev) & 1u)) return hipSuccess;
+  hipLaunchKernelGGL(k_gf16_tables, dim3((65535 + 255) / 256), dim3(256), 0, s);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;  // (once per device: every later stream sees them)
+  if (dev < 64) g_tables_ready |= 1ull << dev;
+  return hipSuccess;
 }
 
 // ============================================================ host push copy
@@ -444,6 +497,8 @@ hipError_t launch_regen_tail_rt(uint32_t k, const SynBatchObj *objs, uint32_t co
 hipError_t launch_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count, hipStream_t s) {
   if (count == 0) return hipSuccess;
   if (k > 64) return hipErrorInvalidValue;
+  const hipError_t te = ensure_gf16_tables(s);
+  if (te != hipSuccess) return te;
   const uint32_t waves = 4, grid = (count + waves - 1) / waves < 8192u ? (count + waves - 1) / waves : 8192u;
   hipLaunchKernelGGL(k_rt_coefs, dim3(grid), dim3(64 * waves), 0, s, k, objs, count);
   return hipGetLastError();

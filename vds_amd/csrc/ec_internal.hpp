@@ -182,7 +182,9 @@ struct SynBatchRt {
 //   c[m][j] = Z(e_m) prod_{i != j} (e_m + b_i) / (Z(b_j) prod_{i != j} (b_j + b_i)):
 // |E| fixed PERM evaluations and |E|^2 runtime products instead of RT's
 // |E| k.  coef holds c (row m, column j < ne) in RT's spread form.
-constexpr uint32_t kRt2MaxRows = 8;  // (one r_j per free LDS slot K..K+7 of the k = 32 kernel)
+// (two groups of r_j through the free LDS slots K..K+7 of the k = 32 kernel;
+// above ~12 rows the |E|^2 products cost more than RT's |E| k)
+constexpr uint32_t kRt2MaxRows = 12;
 struct SynBatchObj {
   const uint8_t *chunks[kMaxFastK];  // survivor j = the chunk of plan point j (K used); RT: of slot j
   uint8_t *out;                      // restore: the object's bytes

@@ -684,7 +684,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
           for (int g = 0; g < 4; ++g) L.put(4 * (int)FillP::kPoint[wave < FillP::kFill ? wave : 0] + g, z);
         }
       }
-      if (rt2_tile) {  // RT2: slot K + wave collects r_j of row j = wave in phase 2
+      if (rt2_tile) {  // RT2: slot K + wave collects r_j of rows j = wave (+ 8) in phase 2
         const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int g = 0; g < 4; ++g) L.put(4 * (K + wave) + g, z);
@@ -857,82 +857,151 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       constexpr int kMC = 2;
       if (rt2_tile) {
         if constexpr (kRt2) {
-          // ---- 2 (RT2, at most 8 rows: slots K..K+7 collect r_j). (a) this
-          // wave's borrowed survivors y_(b_j) into slot K + j (their half's
-          // bits), (b) the PERM program's P0(b_j) of both halves (reads through
-          // c -> c ^ t'_h, merged by half) into the same slots, barrier, (c)
-          // row m = wave: sum_j c[m][j] r_j by the x^b chains of the r_j, (d)
-          // P(e_m) into the erased slots (zero in their halves until now)
+          // ---- 2 (RT2). Rows in groups of 8 (slots K..K+7 collect the
+          // group's r_j): (a) this wave's borrowed survivors y_(b_j) into slot
+          // K + j - g0 (their half's bits; the first group from the stage-1
+          // registers, a second one reloaded from the survivors' bytes, so
+          // the registers do not live across the first group), (b) the PERM
+          // program's P0(b_j) of both halves (reads through c -> c ^ t'_h,
+          // merged by half) into the same slots, barrier, (c) rows m = wave,
+          // wave + 8 accumulate sum_j c[m][j] r_j (two rows per walk of each
+          // r_j's x^b chain); after the last group (d) P(e_m) into the erased
+          // slots (zero in their halves until then: the P0 reads need that)
           const uint8_t *ep0 = d0.rt.epoint, *ep1 = d1.rt.epoint, *sp0 = d0.rt.spoint, *sp1 = d1.rt.spoint;
-          // (a)
+          Plane16 racc[2];
+          racc[0] = plane_zero();
+          racc[1] = plane_zero();
+          const bool two_rows = (uint32_t)wave + 8u < rt_rows;
+          // (a), first group: from the stage-1 registers (dead after this)
 #pragma unroll
           for (int sl = 0; sl < S::kLoadPer; ++sl) {
             const int slot = wave * S::kLoadPer + sl;
 #pragma unroll
             for (int h = 0; h < 2; ++h)
               if ((bor[h] >> slot) & 1u) {
-                const int j = __builtin_popcountll(bor[h] & ((1ull << slot) - 1));
-                Plane16 v;
+                const uint32_t j = (uint32_t)__builtin_popcountll(bor[h] & ((1ull << slot) - 1));
+                if (j < 8u) {
+                  Plane16 v;
 #pragma unroll
-                for (int b = 0; b < 16; ++b) v.p[b] = Ps[sl].p[b] & (h ? vh1 : vh0);
-                lds_xor_point(L, K + j, v);
+                  for (int b = 0; b < 16; ++b) v.p[b] = Ps[sl].p[b] & (h ? vh1 : vh0);
+                  lds_xor_point(L, K + (int)j, v);
+                }
               }
           }
-          // (b)
 #pragma clang loop unroll(disable)
-          for (uint32_t j = 0; j < rt_rows; ++j) {
-            const bool h0 = j < ne0, h1 = j < ne1;
-            const uint32_t t0 = h0 ? s_ld_u8(sp0, (int)s_ld_u8(ep0, (int)j)) - (uint32_t)K : 0u;
-            const uint32_t t1 = h1 ? s_ld_u8(sp1, (int)s_ld_u8(ep1, (int)j)) - (uint32_t)K : 0u;
-            struct Rt2In {
-              const SynLds &L;
-              uint32_t t0, t1, m0, m1;
-              __device__ __forceinline__ u32x4 operator()(int g) const {
-                const u32x4 x0 = L(4 * (int)((uint32_t)(g >> 2) ^ t0) + (g & 3));
-                const u32x4 x1 = L(4 * (int)((uint32_t)(g >> 2) ^ t1) + (g & 3));
-                return (x0 & m0) | (x1 & m1);
+          for (uint32_t g0 = 0; g0 < rt_rows; g0 += 8) {
+            const uint32_t g1 = rt_rows < g0 + 8 ? rt_rows : g0 + 8;
+            // (a), a later group: reloaded
+            if (g0 > 0) {
+              __syncthreads();  // every wave has read the previous group's r_j, (c)
+              const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+              for (int g = 0; g < 4; ++g) L.put(4 * (K + wave) + g, z);
+              __syncthreads();
+#pragma unroll
+              for (int sl = 0; sl < S::kLoadPer; ++sl) {
+                const int slot = wave * S::kLoadPer + sl;
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                  if ((bor[h] >> slot) & 1u) {
+                    const uint32_t j = (uint32_t)__builtin_popcountll(bor[h] & ((1ull << slot) - 1));
+                    if (j >= g0 && j < g1) {
+                      const SynBatchObj &d = half_obj(tile, h);
+                      const uint64_t st0 = half_s0(tile, h);
+                      const int64_t valid = (int64_t)s_ld(&d.chunk_len) - (int64_t)(2 * st0) - 16 * lane;
+                      const uint8_t *src = s_ld(&d.chunks[slot]) + 2 * st0 + 16 * lane;
+                      uint32_t W[16];
+#pragma unroll
+                      for (int q = 0; q < 4; ++q) {
+                        const u32x4 v = (q >> 1) == h ? ld16_guard(src + 1024 * (q & 1), valid - 1024 * (q & 1))
+                                                      : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+                        for (int d4 = 0; d4 < 4; ++d4) W[4 * q + d4] = v[d4];
+                      }
+                      transpose16x2(W, bm);
+                      Plane16 v;
+#pragma unroll
+                      for (int b = 0; b < 16; ++b) v.p[b] = W[b ^ 8] & (h ? vh1 : vh0);
+                      lds_xor_point(L, K + (int)(j - g0), v);
+                    }
+                  }
               }
-            } in{L, t0, t1, h0 ? vh0 : 0u, h1 ? vh1 : 0u};
-            uint32_t pacc[16];
-            PermSyn<K>::part(wave, in, pacc);
-            lds_xor_point(L, K + (int)j, *reinterpret_cast<const Plane16 *>(pacc));
-          }
-          __syncthreads();  // the r_j are whole
-          if ((uint32_t)wave < rt_rows) {
-            // (c)
-            const uint32_t m = (uint32_t)wave;
-            Plane16 racc = plane_zero();
-#pragma clang loop unroll(disable)
-            for (uint32_t j = 0; j < rt_rows; ++j) {
-              const uint32_t c0 = (m < ne0 && j < ne0) ? s_ld(cf0 + (m * K + j)) : 0u;
-              const uint32_t c1 = (m < ne1 && j < ne1) ? s_ld(cf1 + (m * K + j)) : 0u;
-              const uint32_t x = c0 | (c1 << 8);
-              Plane16 tt;
-              syn_get_point(L, K + (int)j, tt.p);
-              static_for<0, 8>([&](auto bp) {
-                constexpr int b = 2 * decltype(bp)::value;
-                __builtin_amdgcn_sched_barrier(0);
-                const Plane16 t1 = plane_mulx(tt);
-                rec_dual_x<b>(racc, tt, t1, x);
-                if constexpr (b < 14) tt = plane_mulx(t1);
-              });
             }
-            // (d)
+            // (b)
+#pragma clang loop unroll(disable)
+            for (uint32_t j = g0; j < g1; ++j) {
+              const bool h0 = j < ne0, h1 = j < ne1;
+              const uint32_t t0 = h0 ? s_ld_u8(sp0, (int)s_ld_u8(ep0, (int)j)) - (uint32_t)K : 0u;
+              const uint32_t t1 = h1 ? s_ld_u8(sp1, (int)s_ld_u8(ep1, (int)j)) - (uint32_t)K : 0u;
+              struct Rt2In {
+                const SynLds &L;
+                uint32_t t0, t1, m0, m1;
+                __device__ __forceinline__ u32x4 operator()(int g) const {
+                  const u32x4 x0 = L(4 * (int)((uint32_t)(g >> 2) ^ t0) + (g & 3));
+                  const u32x4 x1 = L(4 * (int)((uint32_t)(g >> 2) ^ t1) + (g & 3));
+                  return (x0 & m0) | (x1 & m1);
+                }
+              } in{L, t0, t1, h0 ? vh0 : 0u, h1 ? vh1 : 0u};
+              uint32_t pacc[16];
+              PermSyn<K>::part(wave, in, pacc);
+              lds_xor_point(L, K + (int)(j - g0), *reinterpret_cast<const Plane16 *>(pacc));
+            }
+            __syncthreads();  // the group's r_j are whole
+            // (c)
+            if ((uint32_t)wave < rt_rows) {
+#pragma clang loop unroll(disable)
+              for (uint32_t j = g0; j < g1; ++j) {
+                uint32_t x[2];
+#pragma unroll
+                for (int mi = 0; mi < 2; ++mi) {
+                  const uint32_t m = (uint32_t)wave + 8u * mi;
+                  const uint32_t c0 = (m < ne0 && j < ne0) ? s_ld(cf0 + (m * K + j)) : 0u;
+                  const uint32_t c1 = (m < ne1 && j < ne1) ? s_ld(cf1 + (m * K + j)) : 0u;
+                  x[mi] = c0 | (c1 << 8);
+                }
+                Plane16 tt;
+                syn_get_point(L, K + (int)(j - g0), tt.p);
+                if (two_rows) {
+                  static_for<0, 8>([&](auto bp) {
+                    constexpr int b = 2 * decltype(bp)::value;
+                    __builtin_amdgcn_sched_barrier(0);
+                    const Plane16 t1 = plane_mulx(tt);
+                    rec_dual_x<b>(racc[0], tt, t1, x[0]);
+                    rec_dual_x<b>(racc[1], tt, t1, x[1]);
+                    if constexpr (b < 14) tt = plane_mulx(t1);
+                  });
+                } else {
+                  static_for<0, 8>([&](auto bp) {
+                    constexpr int b = 2 * decltype(bp)::value;
+                    __builtin_amdgcn_sched_barrier(0);
+                    const Plane16 t1 = plane_mulx(tt);
+                    rec_dual_x<b>(racc[0], tt, t1, x[0]);
+                    if constexpr (b < 14) tt = plane_mulx(t1);
+                  });
+                }
+              }
+            }
+          }
+          // (d)
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi) {
+            const uint32_t m = (uint32_t)wave + 8u * mi;
+            if (m >= rt_rows) break;
             const int p0 = m < ne0 ? (int)s_ld_u8(ep0, (int)m) : -1;
             const int p1 = m < ne1 ? (int)s_ld_u8(ep1, (int)m) : -1;
             if (p0 >= 0 && p0 == p1) {
-              lds_xor_point(L, p0, racc);
+              lds_xor_point(L, p0, racc[mi]);
             } else {
               if (p0 >= 0) {
                 Plane16 v;
 #pragma unroll
-                for (int b = 0; b < 16; ++b) v.p[b] = racc.p[b] & vh0;
+                for (int b = 0; b < 16; ++b) v.p[b] = racc[mi].p[b] & vh0;
                 lds_xor_point(L, p0, v);
               }
               if (p1 >= 0) {
                 Plane16 v;
 #pragma unroll
-                for (int b = 0; b < 16; ++b) v.p[b] = racc.p[b] & vh1;
+                for (int b = 0; b < 16; ++b) v.p[b] = racc[mi].p[b] & vh1;
                 lds_xor_point(L, p1, v);
               }
             }

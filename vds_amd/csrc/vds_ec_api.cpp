@@ -1570,9 +1570,26 @@ struct SynBatchBuild {
   // nonzero bitmask; 0 marks a free entry)
   std::vector<uint64_t> hkey;
   std::vector<uint32_t> hval;
+  std::vector<uint32_t> hused;  // entries of hkey in use (cleared one by one when the table is reused)
+  std::vector<uint64_t> first_, used_;
+  std::vector<SynBatchPlan> sorted_;  // (batch_begin's class order; swapped with plans)
   unsigned hshift = 64;
 
   static size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
+
+  // A builder is per thread and reused (batch_scratch): the vectors keep
+  // their capacity, so a steady stream of calls allocates nothing.
+  void reset(uint32_t k_, uint32_t n_) {
+    k = k_;
+    n = n_;
+    regen = false;
+    cls_end[0] = cls_end[1] = cls_end[2] = 0;
+    slot = nullptr;
+    cap_objs = cap_tiles = cap_plans = o_tiles = o_plans = 0;
+    objs = nullptr;
+    nobj = 0;
+    plans.clear();
+  }
 
   // The slot bytes for `count` objects of `halves` half tiles; then attach().
   size_t layout(uint32_t count, uint64_t halves) {
@@ -1592,8 +1609,13 @@ struct SynBatchBuild {
     obj_halves.assign(count, 0);
     unsigned bits = 4;
     while ((1ull << bits) < 2ull * count) ++bits;
-    hkey.assign(1ull << bits, 0);
-    hval.assign(1ull << bits, 0);
+    if (hkey.size() != (1ull << bits)) {
+      hkey.assign(1ull << bits, 0);
+      hval.assign(1ull << bits, 0);
+    } else {
+      for (const uint32_t x : hused) hkey[x] = 0;
+    }
+    hused.clear();
     hshift = 64 - bits;
     for (uint32_t &x : perm_idx) x = UINT32_MAX;
   }
@@ -1627,6 +1649,7 @@ struct SynBatchBuild {
     plans.push_back(pl);
     hkey[i] = hk;
     hval[i] = p;
+    hused.push_back((uint32_t)i);
     return p;
   }
   // Descriptor i: survivors in the plan's point order (ascending ids).
@@ -1653,8 +1676,9 @@ struct SynBatchBuild {
     if (nobj == 0) return hip_status(param_release(slot, s));
     const uint32_t empty = nobj;
     std::memset(&objs[empty], 0, sizeof(SynBatchObj));
-    std::vector<uint64_t> first(plans.size() + 1, 0);  // tile offset of each plan
-    std::vector<uint64_t> used(plans.size(), 0);
+    std::vector<uint64_t> &first = first_, &used = used_;
+    first.assign(plans.size() + 1, 0);  // tile offset of each plan
+    used.assign(plans.size(), 0);
     for (uint32_t o = 0; o < nobj; ++o) first[obj_plan[o] + 1] += obj_halves[o];
     for (size_t p = 0; p < plans.size(); ++p) first[p + 1] = first[p] + (first[p + 1] + 1) / 2;
     const uint64_t ntiles = first[plans.size()];
@@ -1752,9 +1776,20 @@ struct RtBatchBuild {
   uint64_t cap_rows = 0;
   SynBatchObj *objs = nullptr;
   uint32_t nobj = 0;
-  std::vector<uint32_t> obj_halves;
+  std::vector<uint32_t> obj_halves, cnt_, order_;
 
   static size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
+
+  void reset(uint32_t k_, uint32_t n_) {  // (reused per thread, as SynBatchBuild)
+    k = k_;
+    n = n_;
+    rt2 = false;
+    slot = nullptr;
+    cap_tiles = o_tiles = o_coef = 0;
+    cap_rows = 0;
+    objs = nullptr;
+    nobj = 0;
+  }
 
   // The slot bytes for `count` descriptors of `halves` half tiles and `rows`
   // coefficient rows; then attach().
@@ -1821,7 +1856,9 @@ struct RtBatchBuild {
     // paired in that order; a tile never pairs the two modes (the kernel's
     // phase 2 is per tile)
     const uint32_t kKeys = kMaxFastK + 1;
-    std::vector<uint32_t> cnt(2 * kKeys + 1, 0), order(nobj);
+    std::vector<uint32_t> &cnt = cnt_, &order = order_;
+    cnt.assign(2 * kKeys + 1, 0);
+    order.resize(nobj);
     auto key = [&](uint32_t o) { return (objs[o].rt.mode == 1u ? 0u : kKeys) + objs[o].rt.ne; };
     for (uint32_t o = 0; o < nobj; ++o) ++cnt[key(o) + 1];
     for (uint32_t r = 1; r < cnt.size(); ++r) cnt[r] += cnt[r - 1];
@@ -1875,6 +1912,8 @@ struct BatchIndex {
   uint64_t syn_halves = 0, rt_halves = 0, rt_rows = 0;
   void build(const std::vector<BatchObjInfo> &info) {
     const uint32_t count = (uint32_t)info.size();
+    nsyn = nrt = 0;
+    syn_halves = rt_halves = rt_rows = 0;
     syn.assign(count, 0);
     rt.assign(count, 0);
     rtrow.assign(count, 0);
@@ -1925,6 +1964,22 @@ struct HostTrace {
 
 // Acquire both builders' slots (together: see param_acquire_n), resolve the
 // syndrome objects' plans (serial: the plan store and the per-call hash).
+// The batch calls' per-object tables, per thread and reused: at 16K objects
+// a call's fresh vectors came from mmap and paid their page faults every
+// call (~100 us of the planning at loss 0.25).
+struct BatchScratch {
+  std::vector<uint64_t> lens;
+  std::vector<BatchObjInfo> info;
+  std::vector<uint32_t> plan;
+  BatchIndex ix;
+  SynBatchBuild bb;
+  RtBatchBuild rb;
+};
+BatchScratch &batch_scratch() {
+  thread_local BatchScratch sc;
+  return sc;
+}
+
 int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, SynBatchBuild &bb, RtBatchBuild &rb,
                 std::vector<uint32_t> &plan, hipStream_t s) {
   size_t bytes[2];
@@ -1965,7 +2020,8 @@ int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, Syn
       order[q] = (uint32_t)p;
       remap[p] = q;
     }
-    std::vector<SynBatchPlan> sorted(np);
+    std::vector<SynBatchPlan> &sorted = bb.sorted_;
+    sorted.resize(np);
     for (size_t q = 0; q < np; ++q) sorted[q] = bb.plans[order[q]];
     bb.plans.swap(sorted);
     for (uint32_t o = 0; o < count; ++o)
@@ -1994,8 +2050,11 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
   HostTrace ht("restore_batch");
   // pass 1 (parallel): every object validated before anything is enqueued,
   // its route and sizes
-  std::vector<uint64_t> lens(count);
-  std::vector<BatchObjInfo> info(count);
+  BatchScratch &sc = batch_scratch();
+  std::vector<uint64_t> &lens = sc.lens;
+  std::vector<BatchObjInfo> &info = sc.info;
+  lens.assign(count, 0);
+  info.assign(count, BatchObjInfo{});
   FirstError err;
   parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
     for (uint32_t o = o0; o < o1; ++o) {
@@ -2035,12 +2094,14 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
   int rc = device_ready();
   if (rc) return rc;
   ht.mark("pass1");
-  BatchIndex ix;
+  BatchIndex &ix = sc.ix;
   ix.build(info);
-  SynBatchBuild bb{k, n};
-  RtBatchBuild rb{k, n};
+  SynBatchBuild &bb = sc.bb;
+  bb.reset(k, n);
+  RtBatchBuild &rb = sc.rb;
+  rb.reset(k, n);
   rb.rt2 = rt2_enabled();  // (restore only; RtBatchBuild::fill decides per object)
-  std::vector<uint32_t> plan;
+  std::vector<uint32_t> &plan = sc.plan;
   ht.mark("index");
   if ((rc = batch_begin(info, ix, bb, rb, plan, s))) return rc;
   ht.mark("begin");
@@ -2096,7 +2157,9 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
   const bool batch_ok = k % 4 == 0 && has_restore_syn(k, n);
   const bool syn = batch_ok && !restore_path_override_bs();
   HostTrace ht("regenerate_batch");
-  std::vector<BatchObjInfo> info(count);
+  BatchScratch &sc = batch_scratch();
+  std::vector<BatchObjInfo> &info = sc.info;
+  info.assign(count, BatchObjInfo{});
   FirstError err;
   parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
     for (uint32_t o = o0; o < o1; ++o) {
@@ -2153,12 +2216,14 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
   for (const BatchObjInfo &f : info)  // (RT descriptors per object: nt / (n - k) rounded up, < 256)
     if (f.route == kRouteRt && (uint32_t)f.parts * R < nt) return VDS_EC_EINVAL;
   ht.mark("pass1");
-  BatchIndex ix;
+  BatchIndex &ix = sc.ix;
   ix.build(info);
-  SynBatchBuild bb{k, n};
+  SynBatchBuild &bb = sc.bb;
+  bb.reset(k, n);
   bb.regen = true;
-  RtBatchBuild rb{k, n};
-  std::vector<uint32_t> plan;
+  RtBatchBuild &rb = sc.rb;
+  rb.reset(k, n);
+  std::vector<uint32_t> &plan = sc.plan;
   ht.mark("index");
   if ((rc = batch_begin(info, ix, bb, rb, plan, s))) return rc;
   ht.mark("begin");

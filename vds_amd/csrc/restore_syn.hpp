@@ -933,15 +933,21 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
               const bool h0 = j < ne0, h1 = j < ne1;
               const uint32_t t0 = h0 ? s_ld_u8(sp0, (int)s_ld_u8(ep0, (int)j)) - (uint32_t)K : 0u;
               const uint32_t t1 = h1 ? s_ld_u8(sp1, (int)s_ld_u8(ep1, (int)j)) - (uint32_t)K : 0u;
+              // half 0's bits read through t0, half 1's through t1, one
+              // v_bitop3 select per word; a half without row j reads the other
+              // half's way (its bits are garbage that no coefficient uses)
               struct Rt2In {
                 const SynLds &L;
-                uint32_t t0, t1, m0, m1;
+                uint32_t t0, t1, sel;
                 __device__ __forceinline__ u32x4 operator()(int g) const {
                   const u32x4 x0 = L(4 * (int)((uint32_t)(g >> 2) ^ t0) + (g & 3));
                   const u32x4 x1 = L(4 * (int)((uint32_t)(g >> 2) ^ t1) + (g & 3));
-                  return (x0 & m0) | (x1 & m1);
+                  u32x4 v;
+#pragma unroll
+                  for (int w = 0; w < 4; ++w) v[w] = __builtin_amdgcn_bitop3_b32(sel, x0[w], x1[w], 0xCA);
+                  return v;
                 }
-              } in{L, t0, t1, h0 ? vh0 : 0u, h1 ? vh1 : 0u};
+              } in{L, h0 ? t0 : t1, h1 ? t1 : t0, vh0};
               uint32_t pacc[16];
               PermSyn<K>::part(wave, in, pacc);
               lds_xor_point(L, K + (int)(j - g0), *reinterpret_cast<const Plane16 *>(pacc));

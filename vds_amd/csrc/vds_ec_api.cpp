@@ -1981,7 +1981,7 @@ BatchScratch &batch_scratch() {
 }
 
 int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, SynBatchBuild &bb, RtBatchBuild &rb,
-                std::vector<uint32_t> &plan, hipStream_t s) {
+                std::vector<uint32_t> &plan, hipStream_t s, HostTrace *ht) {
   size_t bytes[2];
   ParamSlot *sl[2] = {};
   int nb = 0;
@@ -1989,9 +1989,11 @@ int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, Syn
   if (ix.nrt) bytes[nb++] = rb.layout(ix.nrt, ix.rt_halves, ix.rt_rows);
   const hipError_t e = param_acquire_n(nb, bytes, sl);
   if (e != hipSuccess) return hip_status(e);
+  if (ht) ht->mark("acquire");
   nb = 0;
   if (ix.nsyn) bb.attach(sl[nb++]);
   if (ix.nrt) rb.attach(sl[nb++]);
+  if (ht) ht->mark("attach");
   if (ix.nsyn) {
     // One pass resolves every object's plan (first seen, first numbered);
     // then the plans are renumbered class by class -- SMALL ms = 1, ms = 2,
@@ -2008,6 +2010,7 @@ int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, Syn
         if (ix.nrt) rb.abandon(s);
         return VDS_EC_ESINGULAR;
       }
+    if (ht) ht->mark("plans");
     const size_t np = bb.plans.size();
     auto rank = [](uint32_t cls) { return cls == 1 ? 0 : cls == 2 ? 1 : cls == 3 ? 2 : 3; };
     std::vector<uint32_t> order(np), remap(np);
@@ -2103,7 +2106,7 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
   rb.rt2 = rt2_enabled();  // (restore only; RtBatchBuild::fill decides per object)
   std::vector<uint32_t> &plan = sc.plan;
   ht.mark("index");
-  if ((rc = batch_begin(info, ix, bb, rb, plan, s))) return rc;
+  if ((rc = batch_begin(info, ix, bb, rb, plan, s, &ht))) return rc;
   ht.mark("begin");
   // pass 2 (parallel): the descriptors
   parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
@@ -2225,7 +2228,7 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
   rb.reset(k, n);
   std::vector<uint32_t> &plan = sc.plan;
   ht.mark("index");
-  if ((rc = batch_begin(info, ix, bb, rb, plan, s))) return rc;
+  if ((rc = batch_begin(info, ix, bb, rb, plan, s, &ht))) return rc;
   ht.mark("begin");
   parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
     for (uint32_t o = o0; o < o1; ++o) {

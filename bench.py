@@ -155,7 +155,10 @@ def kernel_names(k, n, nodes, size, L, objects):
     ep = _lib.lib().vds_ec_encode16_path(k, ids.ctypes.data_as(_lib.u16p), n, C.c_uint64(size))
     rp = _lib.lib().vds_ec_restore16_path(k, nd.ctypes.data_as(_lib.u16p), C.c_uint64(L), size % (2 * k), objects)
     enc = {2: f"k_encode_bs<{k},{n}>"}.get(ep, "k_encode_generic")
-    rep = {4: f"vds_ec_jit_restore<{k},{n}>", 3: f"k_restore_syn<{k},{n}>", 2: f"k_restore_bs<{k}>"}.get(
+    # the run-time compiled kernel's symbol carries (k, n) and the survivor
+    # mask (vds_ec_jit.cpp kernel_name), as rocprofv3 lists it
+    mask = sum(1 << int(r) for r in nodes)
+    rep = {4: f"vds_ec_jit_restore_{k}_{n}_{mask:x}", 3: f"k_restore_syn<{k},{n}>", 2: f"k_restore_bs<{k}>"}.get(
         rp, "k_restore_generic")
     return enc, rep
 
@@ -170,6 +173,8 @@ def pmc_traffic(path, kernel, objects, k, n):
     except (OSError, ValueError):
         return None, None
     e = t.get(kernel.split("<")[0])
+    if e is None and kernel.startswith("vds_ec_jit_restore"):
+        e = t.get("vds_ec_jit_restore")  # (profiles taken before the kernels carried their survivor set)
     if not e or (e.get("k", 16), e.get("n", 20)) != (k, n):
         return None, None
     return round(e["bytes_per_object"] * objects), f"{os.path.relpath(path, ROOT)}: {e['source']}"

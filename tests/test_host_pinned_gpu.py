@@ -66,3 +66,28 @@ def test_registered_buffer_and_errors(gpu):
         chunk.host_unregister(reps)
     with pytest.raises(VdsEcError):
         chunk.host_unregister(objs)  # no longer registered
+
+
+def test_registered_slabs_on_every_device(gpu):
+    """A registered range's device address is resolved per device (ADVICE r4:
+    the host batches send group g to device g mod ndev, and a mapped host
+    range need not have one address on all of them).  Many small groups over
+    every visible device (max_devices = 8), registered input and output slabs,
+    against the oracle; on a one-GPU box this still runs the lookup path."""
+    from vds_amd import chunk
+    k, n, size, count = 32, 64, 65536, 4096  # 4096 x 64 KiB: several 64 MiB groups
+    L = chunk.replica_size(k, size)
+    objs = np.concatenate([O.splitmix(SEED + 77 + o, size) for o in range(16)] * (count // 16))
+    reps = np.zeros(count * n * L, dtype=np.uint8)
+    chunk.host_register(objs)
+    chunk.host_register(reps)
+    try:
+        outs = [[reps[(o * n + i) * L:(o * n + i + 1) * L] for i in range(n)] for o in range(count)]
+        chunk.encode_host_batch(k, range(n), [objs[o * size:(o + 1) * size] for o in range(count)], outs=outs,
+                                max_devices=8)
+        for o in (0, 1, count // 2 + 3, count - 1):
+            for i in (0, 33, n - 1):
+                assert np.array_equal(outs[o][i], O.encode(k, i, objs[o * size:(o + 1) * size])), (o, i)
+    finally:
+        chunk.host_unregister(objs)
+        chunk.host_unregister(reps)

@@ -6,6 +6,7 @@ index sequence broke every JIT kernel once) fails on the CPU suite instead of
 as silent AOT fallbacks on the GPU box."""
 import os
 import subprocess
+import sys
 
 import pytest
 
@@ -34,3 +35,22 @@ def test_restore_body_compiles_under_hiprtc(tmp_path, regen):
     r = subprocess.run([HELPER, str(src), str(out)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
     assert out.stat().st_size > 0
+
+
+@pytest.mark.skipif(not os.access(HELPER, os.X_OK), reason="vds_ec_jitc not built (run __graft_entry__.build())")
+def test_jit_kernel_symbol_names_its_set(tmp_path):
+    """The run-time kernels are named by kind, (k, n) and survivor mask
+    (vds_ec_jit.cpp kernel_name), so rocprofv3 summaries separate the
+    headline set's kernel from every other instantiation."""
+    code = ("from vds_amd import chunk\n"
+            "print(chunk.jit_build(16, [r for r in range(20) if r not in (0, 5, 10, 15)]))\n")
+    env = dict(os.environ, VDS_EC_JIT_DUMP=str(tmp_path), VDS_EC_JIT_CACHE="0")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    cos = list(tmp_path.glob("*.co"))
+    assert len(cos) == 1
+    notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", str(cos[0])], capture_output=True,
+                           text=True, check=True).stdout
+    mask = sum(1 << r for r in range(20) if r not in (0, 5, 10, 15))
+    assert f".name:           vds_ec_jit_restore_16_20_{mask:x}" in notes or \
+        f"vds_ec_jit_restore_16_20_{mask:x}" in notes

@@ -1,4 +1,4 @@
-"""Summarise tools/pmc_stalls.sh output: mean counter value per launch of the
+"""Summarise tools/runs/pmc_stalls.sh output: mean counter value per launch of the
 named kernel, per variant directory.   python tools/pmc_summary.py KERNEL DIR..."""
 import csv
 import glob

@@ -35,7 +35,7 @@ def main():
     write = per_kernel(f"{wdir}/run_counter_collection.csv", "WRITE_SIZE")
     res = {}
     for name in sorted(set(fetch) & set(write)):
-        if not (name.startswith("k_") or name == "vds_ec_jit_restore") or name == "k_fill_splitmix":
+        if not (name.startswith("k_") or name.startswith("vds_ec_jit_")) or name == "k_fill_splitmix":
             continue
         f2, w = 2 * fetch[name], write[name]
         res[name] = {"bytes_per_object": (f2 + w) / objects, "fetch_bytes_per_object": f2 / objects,

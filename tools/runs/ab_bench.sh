@@ -1,4 +1,4 @@
-# A/B the default library against variant builds: bash tools/ab_bench.sh [variant.so ...]
+# A/B the default library against variant builds: bash tools/runs/ab_bench.sh [variant.so ...]
 # (variants built with vds_amd.build.build(out=..., defines=(...)) and loaded via VDS_EC_LIB)
 cd $GRAFT_REPO_ROOT
 summ() { tail -1 "$1" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$2', 'value',d['value'],'enc',d['encode_GiBps'],'rep',d['repair_GiBps'],'enc_ms',d['encode_ms'],'rep_ms',d['repair_ms'])"; }

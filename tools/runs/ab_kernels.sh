@@ -1,5 +1,5 @@
 # Interleaved A/B of kernel timings (no correctness checks: diagnostic builds
-# allowed): bash tools/ab_kernels.sh ROUNDS variant.so ...   (default lib first)
+# allowed): bash tools/runs/ab_kernels.sh ROUNDS variant.so ...   (default lib first)
 cd $GRAFT_REPO_ROOT
 R=$1; shift
 for i in $(seq $R); do

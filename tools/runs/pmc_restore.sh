@@ -1,4 +1,4 @@
-# SQ / LDS counters for the restore kernel only: bash tools/pmc_restore.sh TAG
+# SQ / LDS counters for the restore kernel only: bash tools/runs/pmc_restore.sh TAG
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp
 D=gpurun_out/pmcr_${1:-x}; mkdir -p $D
 P="rocprofv3 --kernel-trace -f csv"

@@ -1,5 +1,5 @@
 # Stall-breakdown PMC passes for one kernel family, default lib and variants:
-#   bash tools/pmc_stalls.sh encode|restore [variant.so ...]
+#   bash tools/runs/pmc_stalls.sh encode|restore [variant.so ...]
 # Outputs gpurun_out/stall_<tag>/<pass>/ (summarise with tools/pmc_summary.py).
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp

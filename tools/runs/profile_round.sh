@@ -1,6 +1,6 @@
 # Full GPU round: parity suite, PMC traffic passes, the default bench line and
 # its rocprofv3 kernel-trace summary, plus the C4 (k=32) and C5 (host-memory)
-# lines.  Usage: bash tools/profile_round.sh TAG
+# lines.  Usage: bash tools/runs/profile_round.sh TAG
 # Outputs under gpurun_out/prof_TAG/ (copy the summaries into profiles/).
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp

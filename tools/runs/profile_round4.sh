@@ -1,7 +1,7 @@
 # Round-4 GPU pass: parity suite, default bench (headline + C4 + live), its
 # rocprofv3 kernel-trace summary, PMC traffic passes (k=16, k=32), SQ/LDS
 # counters of the k=16 restore, live-shape kernel trace, host bench.
-# Usage: bash tools/profile_round4.sh TAG [PART]   (outputs under gpurun_out/prof_TAG/)
+# Usage: bash tools/runs/profile_round4.sh TAG [PART]   (outputs under gpurun_out/prof_TAG/)
 #   PART a: steps 1-3 (pytest, bench, rocprof bench); b: steps 4-8; default both
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp

@@ -13,7 +13,9 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import fcntl
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -26,10 +28,11 @@ LIB = os.path.join(HERE, "libvds_ec.so")
 JITC = os.path.join(HERE, "vds_ec_jitc")  # the run-time kernel compiler (vds_ec_jitc.cpp), next to the library
 LOCK = os.path.join(HERE, ".build.lock")
 # one translation unit per kernel family, compiled in parallel
-SOURCES = ["ec_generic.hip", "ec_encode.hip", "ec_restore_bs.hip", "ec_restore_syn.hip", "sha256.hip",
-           "vds_ec_api.cpp", "vds_ec_wire.cpp", "vds_ec_jit.cpp"]
+SOURCES = ["ec_encode_16_20.hip", "ec_encode_32_40.hip", "ec_encode_32_64.hip", "ec_restore_syn_32a.hip",
+           "ec_restore_syn_32b.hip", "ec_restore_syn_16.hip", "ec_encode.hip", "ec_restore_syn.hip", "ec_generic.hip",
+           "ec_restore_bs.hip", "sha256.hip", "vds_ec_api.cpp", "vds_ec_wire.cpp", "vds_ec_jit.cpp"]
 HEADERS = ["bitslice.hpp", "gf_common.hpp", "ec_internal.hpp", "ec_device.hpp", "restore_syn.hpp", "xorprog.hpp",
-           "vds_ec_jitc.cpp"]
+           "ec_encode.hpp", "ec_restore_syn.hpp", "vds_ec_jitc.cpp"]
 # The device sources the run-time kernels are compiled from (vds_ec_jit.cpp,
 # hiprtc in the helper vds_ec_jitc), embedded in the helper as jit_embed.inc
 # (written into the build directory).
@@ -90,6 +93,66 @@ def compile_cmd(src: str, obj: str, defines: tuple[str, ...] = (), includes: tup
     return cmd
 
 
+OBJCACHE = os.path.join(HERE, ".objcache")  # compiled objects by content hash (git- and gpurun-ignored)
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _local_includes(path: str, seen: set[str]) -> None:
+    """`path` and every quoted include it reaches under csrc/ or include/."""
+    if path in seen or not os.path.exists(path):
+        return
+    seen.add(path)
+    with open(path, errors="replace") as f:
+        text = f.read()
+    for name in _INC.findall(text):
+        for d in (os.path.dirname(path), CSRC, os.path.join(ROOT, "include")):
+            c = os.path.join(d, name)
+            if os.path.exists(c):
+                _local_includes(c, seen)
+                break
+
+
+def _obj_key(cmd: list[str], src: str) -> str:
+    """Hash of the compile command (minus the output path) and of the bytes of
+    the source and every local header it includes.  A -D define whose macro
+    the unit never names cannot change its object and is left out, so a
+    variant build recompiles only the units its switches reach."""
+    files: set[str] = set()
+    _local_includes(os.path.join(CSRC, src), files)
+    texts = []
+    for f in sorted(files):
+        with open(f, "rb") as fh:
+            texts.append((f, fh.read()))
+    blob = b"".join(t for _, t in texts)
+    args = [a for a in cmd[:-2] if not (a.startswith("-D") and a[2:].split("=")[0].encode() not in blob)]
+    h = hashlib.sha256()
+    h.update("\0".join(args).encode())
+    for f, t in texts:
+        h.update(f.encode())
+        h.update(t)
+    return h.hexdigest()[:32]
+
+
+def _cached_compile(cmd: list[str], obj: str, key: str) -> None:
+    """Compile unless an object with the same key is cached; keep the result."""
+    hit = os.path.join(OBJCACHE, key + ".o")
+    if os.path.exists(hit):
+        shutil.copyfile(hit, obj)
+        return
+    subprocess.run(cmd, check=True)
+    os.makedirs(OBJCACHE, exist_ok=True)
+    tmp = hit + f".{os.getpid()}.tmp"
+    shutil.copyfile(obj, tmp)
+    os.replace(tmp, hit)
+    # bounded: the oldest objects go first
+    ents = sorted((os.path.getmtime(os.path.join(OBJCACHE, e)), e) for e in os.listdir(OBJCACHE) if e.endswith(".o"))
+    for _, e in ents[:-96]:
+        try:
+            os.remove(os.path.join(OBJCACHE, e))
+        except OSError:
+            pass
+
+
 def _compile_all(tmp: str, defines: tuple[str, ...], verbose: bool) -> list[str]:
     jobs = []
     write_jit_embed(tmp)
@@ -98,18 +161,19 @@ def _compile_all(tmp: str, defines: tuple[str, ...], verbose: bool) -> list[str]
         cmd = compile_cmd(src, obj, defines)
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        jobs.append((cmd, obj))
+        jobs.append((cmd, obj, _obj_key(cmd, src)))
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 1), 8))
     rocm = os.path.dirname(os.path.dirname(os.path.realpath(_hipcc())))
     jitc = [_hipcc(), "-O2", "-std=c++20", _arch_define(), "-I", tmp, os.path.join(CSRC, "vds_ec_jitc.cpp"), "-o",
             os.path.join(tmp, "vds_ec_jitc"), f"-L{rocm}/lib", "-lhiprtc", f"-Wl,-rpath,{rocm}/lib",
             "-Wl,--disable-new-dtags"]
     with cf.ThreadPoolExecutor(workers) as ex:
-        futs = [ex.submit(subprocess.run, cmd, check=True) for cmd, _ in jobs]
+        # (SOURCES lists the longest translation units first)
+        futs = [ex.submit(_cached_compile, cmd, obj, key) for cmd, obj, key in jobs]
         futs.append(ex.submit(subprocess.run, jitc, check=True))
         for f in futs:
             f.result()
-    return [obj for _, obj in jobs]
+    return [obj for _, obj, _ in jobs]
 
 
 def build(force: bool = False, verbose: bool = False, out: str | None = None,

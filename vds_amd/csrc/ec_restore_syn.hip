@@ -1,48 +1,27 @@
-// ec_restore_syn.hip -- k_restore_syn<K,N>: restore of an object from any K
-// of its N replicas without a per-pattern K x K inverse
-// (chunk_restore<uint16_t>::restore, chunk.h:290-444; instantiated for
-// (16, 20) and (32, 40), the BASELINE configs).
-//
-// With M = N - K erased points E, per 2048-stripe tile:
-//   1. syndromes S_j = sum_a v_a a^j c_a over all N points (erased = 0): a
-//      fixed map, generated XOR programs (tools/xorgen/gen_restore.cpp);
-//   2. recovery c_E = W_E^{-1} S -- the only runtime arithmetic, M x M;
-//   3. interpolation from the fixed points 0..K-1 (one additive-FFT level +
-//      generated half-size programs + an XOR-only expansion);
-//   4. big-endian stores through an LDS staging of the tile.
-// REGEN stops after step 2 and writes the recovered points as replica bytes:
-// the fused repair of sync_process.cpp:313-335 (decode + re-encode).
-#include <algorithm>
+// ec_restore_syn.hip -- dispatch of k_restore_syn<K,N> (ec_restore_syn.hpp,
+// restore_syn.hpp) to its instantiation units, the run-time compiled
+// survivor-set kernels' launch, and the diagnostic stamp readout.
+#include "ec_restore_syn.hpp"
 
-#include "restore_syn.hpp"
+#include <vector>
 
 namespace vds_ec {
 
-#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#include "generated/restore_16_20_w4.inc"
-#include "generated/restore_32_40_w8.inc"
-#include "generated/smallsyn_16_1.inc"
-#include "generated/smallsyn_16_2.inc"
-#include "generated/smallsyn_32_1.inc"
-#include "generated/smallsyn_32_2.inc"
-#include "generated/permsyn_16.inc"
-#include "generated/permsyn_32.inc"
-#undef VDS_SCHED_FENCE
-
-template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false, class FillP = NoFill>
-__global__ __launch_bounds__((SynShape<K, N, WV>::kThreads), (SynShape<K, N, WV>::kWavesPerSimd))
-void k_restore_syn(SynRestoreArgs a) {
-  restore_syn_body<K, N, WV, REGEN, BATCH, RT, FillP>(a);
-}
-
 #if VDS_DIAG_STAMPS
+// Each instantiation unit is its own code object with its own g_syn_stamps;
+// a run stamps through the kernels of one of them, so the sum is that one.
 extern "C" int vds_ec_diag_stamps(unsigned long long *host, size_t n) {
   if (n > (size_t)kStampSlots) n = kStampSlots;
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_syn_stamps), n * sizeof(unsigned long long));
+  std::vector<unsigned long long> part(n);
+  for (size_t i = 0; i < n; ++i) host[i] = 0;
+  for (auto rd : {syn_stamps_16, syn_stamps_32a, syn_stamps_32b}) {
+    const hipError_t e = rd(part.data(), n);
+    if (e != hipSuccess) return (int)e;
+    for (size_t i = 0; i < n; ++i) host[i] += part[i];
+  }
+  return 0;
 }
 #endif
-
-// =================================================================== launchers
 
 bool has_restore_syn(uint32_t k, uint32_t n) { return (k == 16 && n == 20) || (k == 32 && n == 40); }
 
@@ -52,26 +31,11 @@ const uint16_t *restore_syn_weights(uint32_t k, uint32_t n) {
   return nullptr;
 }
 
-template <int K, int N, int WV, bool REGEN, bool BATCH = false, bool RT = false, class FILL = NoFill>
-static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) {
-  using S = SynShape<K, N, WV>;
-  hipError_t e = ensure_lds_attr(&k_restore_syn<K, N, WV, REGEN, BATCH, RT, FILL>, S::kLdsBytes);
-  if (e != hipSuccess) return e;
-  const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
-  uint32_t grid = 256u * (blocks_per_cu > 0 ? blocks_per_cu : 1);
-  static const uint32_t over = grid_override("VDS_EC_SYN_GRID");
-  if (over) grid = over;
-  if (grid > a.total_tiles) grid = a.total_tiles;
-  if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_restore_syn<K, N, WV, REGEN, BATCH, RT, FILL>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);
-  return hipGetLastError();
-}
-
 hipError_t launch_restore_syn(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen) {
   if (k == 16 && n == 20)
-    return regen ? launch_restore_syn_kn<16, 20, 4, true>(a, s) : launch_restore_syn_kn<16, 20, 4, false>(a, s);
+    return syn_launch_16(SynKind::kPlain, a, s, regen);
   if (k == 32 && n == 40)
-    return regen ? launch_restore_syn_kn<32, 40, 8, true>(a, s) : launch_restore_syn_kn<32, 40, 8, false>(a, s);
+    return syn_launch_32a(SynKind::kPlain, a, s, regen);
   return hipErrorNotSupported;
 }
 
@@ -111,9 +75,9 @@ hipError_t launch_restore_syn_jit(hipFunction_t fn, uint32_t k, uint32_t n, cons
 
 hipError_t launch_restore_syn_batch(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen) {
   if (k == 16 && n == 20)
-    return regen ? launch_restore_syn_kn<16, 20, 4, true, true>(a, s) : launch_restore_syn_kn<16, 20, 4, false, true>(a, s);
+    return syn_launch_16(SynKind::kBatch, a, s, regen);
   if (k == 32 && n == 40)
-    return regen ? launch_restore_syn_kn<32, 40, 8, true, true>(a, s) : launch_restore_syn_kn<32, 40, 8, false, true>(a, s);
+    return syn_launch_32a(SynKind::kBatch, a, s, regen);
   return hipErrorNotSupported;
 }
 
@@ -127,44 +91,30 @@ const uint16_t *restore_small_weights(uint32_t k, uint32_t ms) {
   return nullptr;
 }
 
-template <int K, int N, int WV, int MS>
-static hipError_t launch_small_kn(const SynRestoreArgs &a, hipStream_t s, bool regen) {
-  static_assert(SmallSyn<K, MS>::kSynSlot + MS <= N, "syndrome slots inside the LDS points");
-  return regen ? launch_restore_syn_kn<K, N, WV, true, true, false, SmallSyn<K, MS>>(a, s)
-               : launch_restore_syn_kn<K, N, WV, false, true, false, SmallSyn<K, MS>>(a, s);
-}
-
 hipError_t launch_restore_small_batch(uint32_t k, uint32_t ms, const SynRestoreArgs &a, hipStream_t s, bool regen) {
-  if (k == 16 && ms == 1) return launch_small_kn<16, 20, 4, 1>(a, s, regen);
-  if (k == 16 && ms == 2) return launch_small_kn<16, 20, 4, 2>(a, s, regen);
-  if (k == 32 && ms == 1) return launch_small_kn<32, 40, 8, 1>(a, s, regen);
-  if (k == 32 && ms == 2) return launch_small_kn<32, 40, 8, 2>(a, s, regen);
+  static_assert(SmallSyn<16, 2>::kSynSlot + 2 <= 20 && SmallSyn<32, 2>::kSynSlot + 2 <= 40,
+                "syndrome slots inside the LDS points");
+  const SynKind kind = ms == 1 ? SynKind::kSmall1 : SynKind::kSmall2;
+  if (k == 16 && (ms == 1 || ms == 2)) return syn_launch_16(kind, a, s, regen);
+  if (k == 32 && (ms == 1 || ms == 2)) return syn_launch_32b(kind, a, s, regen);
   return hipErrorNotSupported;
 }
 
 hipError_t launch_regen_perm_batch(uint32_t k, const SynRestoreArgs &a, hipStream_t s) {
-  if (k == 16) return launch_restore_syn_kn<16, 20, 4, true, true, false, PermSyn<16>>(a, s);
-  if (k == 32) return launch_restore_syn_kn<32, 40, 8, true, true, false, PermSyn<32>>(a, s);
+  if (k == 16) return syn_launch_16(SynKind::kPerm, a, s, true);
+  if (k == 32) return syn_launch_32b(SynKind::kPerm, a, s, true);
   return hipErrorNotSupported;
 }
 
 hipError_t launch_restore_multi_batch(uint32_t k, const SynRestoreArgs &a, hipStream_t s, bool regen) {
-  if (k == 16)
-    return regen ? launch_restore_syn_kn<16, 20, 4, true, true, false, MultiP<16>>(a, s)
-                 : launch_restore_syn_kn<16, 20, 4, false, true, false, MultiP<16>>(a, s);
-  if (k == 32)
-    return regen ? launch_restore_syn_kn<32, 40, 8, true, true, false, MultiP<32>>(a, s)
-                 : launch_restore_syn_kn<32, 40, 8, false, true, false, MultiP<32>>(a, s);
+  if (k == 16) return syn_launch_16(SynKind::kMulti, a, s, regen);
+  if (k == 32) return syn_launch_32b(SynKind::kMulti, a, s, regen);
   return hipErrorNotSupported;
 }
 
 hipError_t launch_restore_rt_batch(uint32_t k, uint32_t n, const SynRestoreArgs &a, hipStream_t s, bool regen) {
-  if (k == 16 && n == 20)
-    return regen ? launch_restore_syn_kn<16, 20, 4, true, true, true>(a, s)
-                 : launch_restore_syn_kn<16, 20, 4, false, true, true>(a, s);
-  if (k == 32 && n == 40)
-    return regen ? launch_restore_syn_kn<32, 40, 8, true, true, true>(a, s)
-                 : launch_restore_syn_kn<32, 40, 8, false, true, true>(a, s);
+  if (k == 16 && n == 20) return syn_launch_16(SynKind::kRt, a, s, regen);
+  if (k == 32 && n == 40) return syn_launch_32a(SynKind::kRt, a, s, regen);
   return hipErrorNotSupported;
 }
 

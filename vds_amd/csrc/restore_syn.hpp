@@ -247,6 +247,16 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
 #ifndef VDS_GM2_PRIO
 #define VDS_GM2_PRIO 9
 #endif
+#ifndef VDS_K32_EARLY
+#define VDS_K32_EARLY 0
+#endif
+// One workgroup per CU (k = 32): the second-dispatched half of the waves
+// (wave >= WV / 2) loses VALU arbitration to the older half by age and lags
+// in every phase (profiles/round4/ablog/l2_touch_k32_stamps.txt); with
+// VDS_HALF_PRIO it runs at priority 1 for the whole kernel.
+#ifndef VDS_HALF_PRIO
+#define VDS_HALF_PRIO 0
+#endif
 template <int K, int N, int WV, int W>
 __device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
   using P = RestorePrograms<K, N, WV>;
@@ -544,6 +554,8 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const BitMasks bm = bit_masks();
+  if constexpr (!kPrio && VDS_HALF_PRIO)
+    if (wave >= WV / 2) __builtin_amdgcn_s_setprio(1);
   SynLds L;
   L.base = (lds_char *)lds;
   L.lo = 16u * lane;
@@ -625,7 +637,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   // the programs either)
   // (RT: this wave's slots stay in registers through phase 2; the regenerate
   // branch issues its prefetch there)
-  constexpr bool kLateLoad = ((K == 32 || BATCH) && !REGEN) || RT;
+  constexpr bool kLateLoad = (((K == 32 && !(FILL && VDS_K32_EARLY)) || BATCH) && !REGEN) || RT;
   const uint32_t t_step = tr.step;
   prefetch(tr.first);
   // vmcnt counts loads and stores together and retires them in issue order.

@@ -2285,10 +2285,14 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
 // one contiguous slab skips the staging copies: the H2D DMA reads the
 // caller's bytes, and the push kernel writes the results straight into the
 // caller's pages.  Lookups are per group, not per object.
+constexpr int kPinnedMaxDev = 64;
 struct PinnedRange {
   uint64_t bytes;
-  uint8_t *dev;  // the device address of the range's first byte
-  bool owned;    // vds_ec_host_alloc (freed by vds_ec_host_free) vs registered
+  bool owned;  // vds_ec_host_alloc (freed by vds_ec_host_free) vs registered
+  // the device address of the range's first byte, per device: resolved on
+  // each device the first time a host batch there uses the range (a mapped
+  // host range need not have the same address on every device)
+  uint8_t *dev[kPinnedMaxDev] = {};
 };
 struct PinnedRegistry {
   std::mutex mu;
@@ -2298,8 +2302,9 @@ PinnedRegistry &pinned_registry() {
   static PinnedRegistry *r = new PinnedRegistry();  // never freed: outlives every caller
   return *r;
 }
-// The device address of host bytes [p, p + len) when they lie in one pinned
-// range, else nullptr.
+// The address, on the calling thread's current device, of host bytes
+// [p, p + len) when they lie in one pinned range, else nullptr (then the
+// caller stages the bytes as for pageable memory).
 uint8_t *pinned_device_ptr(const void *p, uint64_t len) {
   if (!p) return nullptr;
   PinnedRegistry &r = pinned_registry();
@@ -2310,7 +2315,15 @@ uint8_t *pinned_device_ptr(const void *p, uint64_t len) {
   if (it == r.ranges.begin()) return nullptr;
   --it;
   if (a + len > it->first + it->second.bytes) return nullptr;
-  return it->second.dev + (a - it->first);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kPinnedMaxDev) return nullptr;
+  uint8_t *&d = it->second.dev[dev];
+  if (!d) {
+    void *q = nullptr;
+    if (hipHostGetDevicePointer(&q, reinterpret_cast<void *>(it->first), 0) != hipSuccess || !q) return nullptr;
+    d = static_cast<uint8_t *>(q);
+  }
+  return d + (a - it->first);
 }
 
 // The D2H of a pinned slab by the push kernel (default) or by the copy
@@ -2987,9 +3000,12 @@ int vds_ec_host_alloc(uint64_t bytes, void **ptr) {
     (void)hipHostFree(p);
     return VDS_EC_EHIP;
   }
+  PinnedRange pr{bytes, true};
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kPinnedMaxDev) pr.dev[dev] = static_cast<uint8_t *>(d);
   PinnedRegistry &r = pinned_registry();
   std::lock_guard<std::mutex> g(r.mu);
-  r.ranges[reinterpret_cast<uintptr_t>(p)] = PinnedRange{bytes, static_cast<uint8_t *>(d), true};
+  r.ranges[reinterpret_cast<uintptr_t>(p)] = pr;
   *ptr = p;
   return VDS_EC_OK;
 }
@@ -3016,9 +3032,12 @@ int vds_ec_host_register(void *ptr, uint64_t bytes) {
     (void)hipHostUnregister(ptr);
     return VDS_EC_EHIP;
   }
+  PinnedRange pr{bytes, false};
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kPinnedMaxDev) pr.dev[dev] = static_cast<uint8_t *>(d);
   PinnedRegistry &r = pinned_registry();
   std::lock_guard<std::mutex> g(r.mu);
-  r.ranges[reinterpret_cast<uintptr_t>(ptr)] = PinnedRange{bytes, static_cast<uint8_t *>(d), false};
+  r.ranges[reinterpret_cast<uintptr_t>(ptr)] = pr;
   return VDS_EC_OK;
 }
 

@@ -52,6 +52,12 @@ extern char **environ;
 #ifndef VDS_GM2_PRIO
 #define VDS_GM2_PRIO 9
 #endif
+#ifndef VDS_K32_EARLY
+#define VDS_K32_EARLY 0
+#endif
+#ifndef VDS_HALF_PRIO
+#define VDS_HALF_PRIO 0
+#endif
 #ifndef VDS_EC_ARCH_STR
 #define VDS_EC_ARCH_STR "gfx950"  // (build.py passes the library's architecture)
 #endif
@@ -127,6 +133,16 @@ struct Entry {
   std::atomic<hipFunction_t> fn[kJitMaxDev] = {};
 };
 
+// The kernel's symbol: kind, (k, n) and the survivor mask, so that profiler
+// summaries (rocprofv3 --stats) tell the instantiations apart, e.g.
+// vds_ec_jit_restore_16_20_f7bde (survivors {1..4, 6..9, 11..14, 16..19}).
+std::string kernel_name(const Key &key) {
+  char b[96];
+  std::snprintf(b, sizeof b, "vds_ec_jit_%s_%u_%u_%llx", key.regen ? "regen" : "restore", key.k, key.n,
+                (unsigned long long)key.survivors);
+  return b;
+}
+
 // The kernel source for one survivor set.
 std::string kernel_source(const Key &key) {
   const int K = (int)key.k, N = (int)key.n, WV = K / 4;
@@ -135,8 +151,8 @@ std::string kernel_source(const Key &key) {
     if ((key.survivors >> a) & 1u) sp.push_back(a);
   std::string s;
   xorgen::appendf(s,
-                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n", VDS_GM2,
-                  VDS_GM2_PRIO);  // (the forms this library was built with)
+                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n#define VDS_K32_EARLY %d\n#define VDS_HALF_PRIO %d\n",
+                  VDS_GM2, VDS_GM2_PRIO, VDS_K32_EARLY, VDS_HALF_PRIO);  // (the forms this library was built with)
   xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
   xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
   if (key.regen) {  // every erased point, in ascending order (= SynRestoreArgs::erased)
@@ -153,9 +169,9 @@ std::string kernel_source(const Key &key) {
   xorgen::appendf(s,
                   "extern \"C\" __global__ __launch_bounds__((vds_ec::SynShape<%d, %d, %d>::kThreads), "
                   "(vds_ec::SynShape<%d, %d, %d>::kWavesPerSimd))\n"
-                  "void vds_ec_jit_restore(vds_ec::SynRestoreArgs a) {\n"
+                  "void %s(vds_ec::SynRestoreArgs a) {\n"
                   "  vds_ec::restore_syn_body<%d, %d, %d, %s, false, false, vds_ec::JitFill>(a);\n}\n",
-                  K, N, WV, K, N, WV, K, N, WV, key.regen ? "true" : "false");
+                  K, N, WV, K, N, WV, kernel_name(key).c_str(), K, N, WV, key.regen ? "true" : "false");
   return s;
 }
 
@@ -407,7 +423,7 @@ class Jit {
     hipModule_t m = nullptr;
     hipFunction_t f = nullptr;
     if (hipModuleLoadData(&m, e->code.data()) != hipSuccess ||
-        hipModuleGetFunction(&f, m, "vds_ec_jit_restore") != hipSuccess) {
+        hipModuleGetFunction(&f, m, kernel_name(key).c_str()) != hipSuccess) {
       if (m) (void)hipModuleUnload(m);
       // remembered (the syndrome kernel serves the set from now on), and the
       // cached file that gave it is dropped so the next process recompiles

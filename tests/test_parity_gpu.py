@@ -657,3 +657,33 @@ def test_host_batches_pack_groups(ec, k, n):
     got = ec.restore_host_batch(k, nodes, [[reps[o][r] for r in nd] for o, nd in enumerate(nodes)])
     for g, d in zip(got, objs):
         assert np.array_equal(g, d), d.size
+
+
+@pytest.mark.parametrize("jit", [0, 2], ids=["aot", "jit"])
+def test_c4_full_size_golden(ec, jit):
+    """BASELINE configs[3] at full size (k = 32, n = 40, one 64 MiB object):
+    every replica of the device encode against the oracle's SHA-256s, and the
+    device repair from the C4 survivors {r : r mod 5 != 0} -- the syndrome
+    kernel k_restore_syn<32,40> (jit 0) and the survivor set's run-time
+    compiled kernel (jit 2, compiled synchronously) -- against the oracle's
+    restore (chunk.h:245-281, 402-444; tests/golden/make_golden.py)."""
+    import torch
+    from vds_amd import chunk
+    enc = next(e for e in G["encode16_sha"] if (e["k"], e["n"], e["size"]) == (32, 40, 64 << 20))
+    rest = next(e for e in G["restore16"] if (e["k"], e["size"]) == (32, 64 << 20))
+    k, n, size = 32, 40, 64 << 20
+    assert rest["nodes"] == [r for r in range(n) if r % 5][:k]
+    t = dev_object(torch, size, enc["object_index"])
+    out = dev_encode(torch, k, n, t, size)
+    for r in range(n):
+        assert sha(out[r, 0].cpu().numpy()) == enc["sha256"][str(r)], f"replica {r}"
+    L = out.shape[2]
+    chunk.jit_set_mode(jit)
+    try:
+        res = torch.full((size,), 0xA5, dtype=torch.uint8, device="cuda")
+        chunk.restore_device(k, rest["nodes"], [out[r, 0].data_ptr() for r in rest["nodes"]], L, L, 0, 1, res, size)
+        torch.cuda.synchronize()
+        assert _path(k, rest["nodes"], L) == (4 if jit else 3)  # (sync mode: compiled at that first use)
+        assert sha(res.cpu().numpy()) == rest["sha256"]
+    finally:
+        chunk.jit_set_mode(0)

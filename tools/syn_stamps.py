@@ -1,7 +1,10 @@
 """Per-phase cycle breakdown of k_restore_syn from the VDS_DIAG_STAMPS build.
 
-  python -c "from vds_amd import build as b; b.build(out='build/stamps.so', defines=('-DVDS_DIAG_STAMPS=1',))"
-  VDS_EC_LIB=build/stamps.so python tools/syn_stamps.py [--objects 128] [--k 32]
+  python -c "from vds_amd import build as b; b.build(out='ab/stamps/libvds_ec.so', defines=('-DVDS_DIAG_STAMPS=1',))"
+  VDS_EC_LIB=ab/stamps/libvds_ec.so python tools/syn_stamps.py [--objects 128] [--k 32] [--jit]
+
+--jit: the survivor set's run-time compiled kernel (compiled synchronously,
+stamps read from its own module) instead of the syndrome kernel.
 
 Each wave sums s_memtime deltas per phase over its tiles; this prints the
 mean per tile of every phase, per wave and overall (barrier phases are the
@@ -26,7 +29,12 @@ NPH = 20
 p = argparse.ArgumentParser()
 p.add_argument("--objects", type=int, default=128)
 p.add_argument("--k", type=int, default=16, choices=(16, 32))
+p.add_argument("--jit", action="store_true")
 a = p.parse_args()
+if a.jit:  # phases of the fill + two-level interpolation kernel (restore_syn.hpp marks)
+    PHASES = ["stage1 transposes+puts", "B1", "-", "-", "-", "scatter fill", "B(fill)", "S1 (levels 1-2)", "B(S1)",
+              "S2 (families)", "B(S2)", "S3 + puts", "B(S3)", "stage C", "B(stage C read) + late loads",
+              "staging transposes+writes", "B(staging)", "copy-out stores", "B(tile end)", "-"]
 k, n, size = a.k, a.k + a.k // 4, 64 << 20
 WV = 4 if k == 16 else 8
 L = chunk.replica_size(k, size)
@@ -38,12 +46,18 @@ for i in range(a.objects):
 nodes = [r for r in range(n) if r % 5 != 0 or r >= 5 * (n - k)][:k]
 chunk.encode_device(k, list(range(n)), inp, size, size, a.objects, [reps[i].data_ptr() for i in range(n)], L)
 cp = [reps[r].data_ptr() for r in nodes]
+chunk.jit_set_mode(2 if a.jit else 0)
 for _ in range(2):
     chunk.restore_device(k, nodes, cp, L, L, size % (2 * k), a.objects, out, size)
 torch.cuda.synchronize()
 lib = _lib.lib()
 buf = np.zeros(4096 * 4 * NPH, dtype=np.uint64)
-rc = lib.vds_ec_diag_stamps(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), C.c_size_t(buf.size))
+if a.jit:
+    nd = np.asarray(nodes, dtype=np.uint16)
+    rc = lib.vds_ec_diag_jit_stamps(C.c_uint16(k), nd.ctypes.data_as(C.POINTER(C.c_uint16)),
+                                    buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), C.c_size_t(buf.size))
+else:
+    rc = lib.vds_ec_diag_stamps(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), C.c_size_t(buf.size))
 assert rc == 0, rc
 grid = 512 if k == 16 else 256
 total_tiles = a.objects * size // (2048 * 2 * k)

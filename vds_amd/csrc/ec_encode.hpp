@@ -18,10 +18,6 @@
 
 namespace vds_ec {
 
-#ifndef VDS_HALF_PRIO
-#define VDS_HALF_PRIO 0  // (restore_syn.hpp: the second-dispatched half of a one-per-CU workgroup at priority 1)
-#endif
-
 // VALU cost of one row-form Horner step for replica r (bitslice.hpp): used
 // to balance replicas across waves.
 constexpr int horner_cost(int r) { return r == 0 ? 1 : row_horner_cost((uint32_t)r); }
@@ -194,13 +190,6 @@ struct EncodeShape {
   static_assert(K % 4 == 0 && WV == K / 4, "fast encode: k % 4 == 0 and k/4 waves");
   static_assert(RPW * WV >= N, "every replica needs a wave");
   __device__ __forceinline__ static constexpr int cell_off(int c) { return 16 * c + kGroupPad * (c >> 2); }
-  // one workgroup per CU (k = 32): VDS_HALF_PRIO gives the second-dispatched
-  // half of the waves (W >= WV / 2) priority 1 for the whole kernel
-  static constexpr bool kOneWg = 2 * kLdsBytes > 160 * 1024;
-  template <int W>
-  static constexpr int base_prio() {
-    return (kOneWg && VDS_HALF_PRIO && W >= WV / 2) ? 1 : 0;
-  }
 };
 
 // Replica r's output pointer, read from the kernel arguments where it is used.
@@ -311,10 +300,10 @@ __device__ __forceinline__ void store_rep(const Plane16 &acc, uint8_t *rep, cons
 // encode 1881-1895 -> 1917-1918 GiB/s), so one wave's store stream is not
 // starved by the other workgroup's Horner.
 constexpr int kEncStorePrio = 2;
-template <int P>
-__device__ __forceinline__ void set_prio() {
-  __builtin_amdgcn_s_setprio(P);
-}
+// (k = 32, one workgroup per CU: the second-dispatched half of the waves at
+// priority 1 for the whole kernel -- as the k = 32 restore does -- measured
+// slower, C4 encode 9.48-9.53 -> 10.38-10.46 ms at 256 x 64 MiB, round 5.)
+
 
 // Replicas evaluated per pass over the tile's cells.  A/B at k = 16 with the
 // non-temporal, prioritised stores (512 objects, 2 rounds): 1 -> 1740, 2 ->
@@ -369,7 +358,7 @@ __device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const Fa
     if (r == 0) store_rep<S::kMap, ST>(xa, rep_ptr(a, 0), a, tp, lane, bm);
     if (r > 0) store_rep<S::kMap, ST>(A[s], rep_ptr(a, r), a, tp, lane, bm);
   }
-  set_prio<S::template base_prio<W>()>();
+  __builtin_amdgcn_s_setprio(0);
 }
 
 template <int K, int N, int RPW, int WV, int W, bool ST, int S0 = 0>
@@ -524,7 +513,7 @@ __device__ __forceinline__ void encode_pair_group(const uint32_t *set_planes, co
       };
       (one(std::integral_constant<int, (int)I>{}), ...);
     }(std::make_index_sequence<PP>{});
-    set_prio<S::template base_prio<W>()>();
+    __builtin_amdgcn_s_setprio(0);
     encode_pair_group<K, N, RPW, WV, W, ST, S0 + PP>(set_planes, a, tp, lane, bm);
   }
 }
@@ -648,7 +637,7 @@ __device__ __forceinline__ void encode_quad_group(const uint32_t *set_planes, co
       const Plane16 r2 = plane_horner_enc<(uint32_t)(4 * j + 2)>(p1y1, p0y1);
       store_rep<S::kMap, ST>(r2, rep_ptr(a, 4 * j + 2), a, tp, lane, bm);
       store_rep<S::kMap, ST>(plane_xor(r2, p1y1), rep_ptr(a, 4 * j + 3), a, tp, lane, bm);
-      set_prio<S::template base_prio<W>()>();
+      __builtin_amdgcn_s_setprio(0);
     }
     encode_quad_group<K, N, RPW, WV, W, ST, S0 + 1>(set_planes, a, tp, lane, bm);
   }
@@ -758,8 +747,6 @@ void k_encode_bs(FastEncodeArgs a) {
   uint32_t *t_planes = lds + tset * S::kSetWords + S::cell_off(4 * tp);
   uint32_t *my_set = lds + lane * S::kSetWords;
   const BitMasks bm = bit_masks();
-  if constexpr (S::kOneWg && VDS_HALF_PRIO)
-    if (wave >= WV / 2) __builtin_amdgcn_s_setprio(1);
 
   constexpr bool kLoad16 = S::kMap != 0;
   u32x2 P[kLoad16 ? 1 : 32];

@@ -247,15 +247,15 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
 #ifndef VDS_GM2_PRIO
 #define VDS_GM2_PRIO 9
 #endif
-#ifndef VDS_K32_EARLY
-#define VDS_K32_EARLY 0
-#endif
 // One workgroup per CU (k = 32): the second-dispatched half of the waves
 // (wave >= WV / 2) loses VALU arbitration to the older half by age and lags
-// in every phase (profiles/round4/ablog/l2_touch_k32_stamps.txt); with
-// VDS_HALF_PRIO it runs at priority 1 for the whole kernel.
+// in every phase (profiles/round4/ablog/l2_touch_k32_stamps.txt), so it runs
+// at priority 1 for the whole kernel.  Same box, C4 at 256 x 64 MiB, three
+// interleaved rounds (profiles/round5/ab_halfprio.log): survivor-set kernel
+// 10.03-10.16 -> 9.83-9.89 ms, k_restore_syn<32,40> 12.33-12.40 -> 12.26-12.32.
+// VDS_HALF_PRIO=0 is the A/B switch.
 #ifndef VDS_HALF_PRIO
-#define VDS_HALF_PRIO 0
+#define VDS_HALF_PRIO 1
 #endif
 template <int K, int N, int WV, int W>
 __device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
@@ -637,7 +637,9 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   // the programs either)
   // (RT: this wave's slots stay in registers through phase 2; the regenerate
   // branch issues its prefetch there)
-  constexpr bool kLateLoad = (((K == 32 && !(FILL && VDS_K32_EARLY)) || BATCH) && !REGEN) || RT;
+  // (the survivor-set kernel at k = 32 with the early issue, after the fill:
+  // 90 VGPRs spilled, round 5 tools/jit_dump.py)
+  constexpr bool kLateLoad = ((K == 32 || BATCH) && !REGEN) || RT;
   const uint32_t t_step = tr.step;
   prefetch(tr.first);
   // vmcnt counts loads and stores together and retires them in issue order.

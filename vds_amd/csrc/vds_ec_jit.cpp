@@ -52,11 +52,11 @@ extern char **environ;
 #ifndef VDS_GM2_PRIO
 #define VDS_GM2_PRIO 9
 #endif
-#ifndef VDS_K32_EARLY
-#define VDS_K32_EARLY 0
-#endif
 #ifndef VDS_HALF_PRIO
-#define VDS_HALF_PRIO 0
+#define VDS_HALF_PRIO 1
+#endif
+#ifndef VDS_DIAG_STAMPS
+#define VDS_DIAG_STAMPS 0
 #endif
 #ifndef VDS_EC_ARCH_STR
 #define VDS_EC_ARCH_STR "gfx950"  // (build.py passes the library's architecture)
@@ -151,8 +151,11 @@ std::string kernel_source(const Key &key) {
     if ((key.survivors >> a) & 1u) sp.push_back(a);
   std::string s;
   xorgen::appendf(s,
-                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n#define VDS_K32_EARLY %d\n#define VDS_HALF_PRIO %d\n",
-                  VDS_GM2, VDS_GM2_PRIO, VDS_K32_EARLY, VDS_HALF_PRIO);  // (the forms this library was built with)
+                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n#define VDS_HALF_PRIO %d\n", VDS_GM2,
+                  VDS_GM2_PRIO, VDS_HALF_PRIO);  // (the forms this library was built with)
+#if VDS_DIAG_STAMPS
+  xorgen::appendf(s, "#define VDS_DIAG_STAMPS 1\n");  // (phase stamps: vds_ec_diag_jit_stamps)
+#endif
   xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
   xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
   if (key.regen) {  // every erased point, in ascending order (= SynRestoreArgs::erased)
@@ -449,6 +452,23 @@ class Jit {
     idle_cv_.wait(lk, [&] { return queue_.empty() && busy_ == 0; });
   }
 
+#if VDS_DIAG_STAMPS
+  // The module of `key` on the current device (diagnostic stamps readout).
+  hipModule_t module(const Key &key) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kJitMaxDev) return nullptr;
+    std::shared_ptr<Entry> e;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = map_.find(key);
+      if (it == map_.end()) return nullptr;
+      e = it->second;
+    }
+    std::lock_guard<std::mutex> g(load_mu_);
+    return e->mod[dev];
+  }
+#endif
+
   // Compile-only (no device): the code object size of `key`'s kernel.
   bool build(const Key &key, size_t *bytes, std::string *log) {
     std::vector<char> code;
@@ -564,6 +584,22 @@ int vds_ec_jit_build16(uint16_t k, const uint16_t *nodes, uint64_t *code_bytes) 
   if (code_bytes) *code_bytes = bytes;
   return VDS_EC_OK;
 }
+
+#if VDS_DIAG_STAMPS
+// Diagnostic build: the phase stamps (restore_syn.hpp Stamps) of survivor set
+// `nodes`' run-time kernel, from its module's own g_syn_stamps.
+int vds_ec_diag_jit_stamps(uint16_t k, const uint16_t *nodes, unsigned long long *host, size_t n) {
+  Key key;
+  if (jit_key(k, nodes, &key)) return VDS_EC_EINVAL;
+  hipModule_t m = Jit::get().module(key);
+  if (!m) return VDS_EC_EINVAL;
+  hipDeviceptr_t d = nullptr;
+  size_t bytes = 0;
+  if (hipModuleGetGlobal(&d, &bytes, m, "_ZN6vds_ec12g_syn_stampsE") != hipSuccess) return VDS_EC_EHIP;
+  if (n * sizeof(unsigned long long) > bytes) n = bytes / sizeof(unsigned long long);
+  return hipMemcpyDtoH(host, d, n * sizeof(unsigned long long)) == hipSuccess ? VDS_EC_OK : VDS_EC_EHIP;
+}
+#endif
 
 int vds_ec_jit_ready16(uint16_t k, const uint16_t *nodes) {
   Key key;

@@ -247,6 +247,12 @@ int vds_ec_restore16_host_split(uint16_t k, const uint16_t *nodes, const uint8_t
  * digests + 32*j (device memory).                                             */
 int vds_ec_sha256_device(const uint8_t *base, uint64_t len, uint64_t stride, uint32_t count, uint8_t *digests,
                          void *stream);
+/* SHA-256 of ONE host message on the calling thread (no GPU): upload_data's
+ * body hash (server_api.cpp:16) is a single chain of dependent compressions,
+ * ~3 us a block in one GPU lane, so vds_ec_save_temp16_host computes it here
+ * while the device encodes and names the replicas.  x86 SHA extensions when
+ * the CPU has them (VDS_EC_HOST_SHA=portable forces the portable code).     */
+int vds_ec_sha256_host(const uint8_t *data, uint64_t len, uint8_t *digest);
 /* vds_ec_encode16_host plus the SHA-256 of every replica, computed on the
  * device before the copy-back: digests receives n*32 bytes (host).          */
 int vds_ec_encode16_hash_host(uint16_t k, const uint16_t *replicas, uint32_t n, const uint8_t *data, uint64_t size,
@@ -283,10 +289,11 @@ int vds_ec_tmp_names(const uint8_t *digests, uint32_t count, char *out);
  * queries the length (excluding the NUL).                                   */
 int vds_ec_upload_response_json(int id, const uint8_t *replica_digests, uint32_t n, const uint8_t *data_digest,
                                  uint32_t replica_size, char *out, size_t cap, size_t *out_len);
-/* save_temp + upload_data's hashing on the device: replicas 0..n-1 of the
- * body (host, size bytes) into outs (n host buffers of vds_ec_replica_size
- * bytes), their SHA-256 names into replica_digests (n*32 host bytes), the
- * body's SHA-256 into data_digest (32 host bytes).                          */
+/* save_temp + upload_data's hashing: replicas 0..n-1 of the body (host,
+ * size bytes) into outs (n host buffers of vds_ec_replica_size bytes), their
+ * SHA-256 names into replica_digests (n*32 host bytes) -- encode and names on
+ * the device --, the body's SHA-256 into data_digest (32 host bytes),
+ * computed on the calling thread meanwhile (vds_ec_sha256_host).            */
 int vds_ec_save_temp16_host(uint16_t k, uint32_t n, const uint8_t *data, uint64_t size, uint8_t *const *outs,
                             uint8_t *replica_digests, uint8_t *data_digest, uint32_t *replica_size);
 

@@ -68,6 +68,7 @@ SIGNATURES = {
     "vds_ec_regenerate16_host": (C.c_int, [C.c_uint16, u16p, vpp, C.c_uint64, u16p, C.c_uint32, vpp]),
     "vds_ec_regenerate16_path": (C.c_int, [C.c_uint16, u16p, u16p, C.c_uint32, C.c_uint64]),
     "vds_ec_sha256_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
+    "vds_ec_sha256_host": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p]),
     "vds_ec_encode16_hash_host": (C.c_int, [C.c_uint16, u16p, C.c_uint32, C.c_void_p, C.c_uint64, vpp, C.c_void_p,
                                             C.c_uint]),
     "vds_ec_replica_paths": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),

@@ -30,7 +30,8 @@ LOCK = os.path.join(HERE, ".build.lock")
 # one translation unit per kernel family, compiled in parallel
 SOURCES = ["ec_encode_16_20.hip", "ec_encode_32_40.hip", "ec_encode_32_64.hip", "ec_restore_syn_32a.hip",
            "ec_restore_syn_32b.hip", "ec_restore_syn_16.hip", "ec_encode.hip", "ec_restore_syn.hip", "ec_generic.hip",
-           "ec_restore_bs.hip", "sha256.hip", "vds_ec_api.cpp", "vds_ec_wire.cpp", "vds_ec_jit.cpp"]
+           "ec_restore_bs.hip", "sha256.hip", "vds_ec_api.cpp", "vds_ec_wire.cpp", "vds_ec_jit.cpp", "sha256_host.cpp"]
+HOST_ONLY = {"sha256_host.cpp"}
 HEADERS = ["bitslice.hpp", "gf_common.hpp", "ec_internal.hpp", "ec_device.hpp", "restore_syn.hpp", "xorprog.hpp",
            "ec_encode.hpp", "ec_restore_syn.hpp", "vds_ec_jitc.cpp"]
 # The device sources the run-time kernels are compiled from (vds_ec_jit.cpp,
@@ -88,7 +89,10 @@ def compile_cmd(src: str, obj: str, defines: tuple[str, ...] = (), includes: tup
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-c", *defines, _arch_define(),
            "-I", os.path.join(ROOT, "include"), *[a for d in includes for a in ("-I", d)],
            os.path.join(CSRC, src), "-o", obj]
-    if src.endswith(".cpp"):
+    if src in HOST_ONLY:  # plain C++ (x86 intrinsics): no device pass
+        cmd = [a for a in cmd if not a.startswith("--offload-arch")]
+        cmd[1:1] = ["-x", "c++"]
+    elif src.endswith(".cpp"):
         cmd[1:1] = ["-x", "hip"]
     return cmd
 

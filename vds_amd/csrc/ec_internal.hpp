@@ -300,6 +300,8 @@ hipError_t launch_restore_generic(const GenericRestoreArgs &a, hipStream_t s);
 // Returns hipErrorNotSupported when no bit-sliced instantiation exists for (k, n).
 hipError_t launch_encode_fast(uint32_t k, uint32_t n, const FastEncodeArgs &a, hipStream_t s);
 bool has_encode_fast(uint32_t k, uint32_t n);
+// SHA-256 of one message on the calling CPU thread (sha256_host.cpp)
+void sha256_host(const uint8_t *data, uint64_t len, uint8_t out[32]);
 hipError_t launch_restore_fast(uint32_t k, const FastRestoreArgs &a, hipStream_t s, bool regen = false);
 bool has_restore_fast(uint32_t k);
 // SHA-256 of count messages of len bytes at base + j * stride -> digests + 32 j (sha256.hip).

@@ -3142,14 +3142,11 @@ int vds_ec_save_temp16_host(uint16_t k, uint32_t n, const uint8_t *data, uint64_
   HostCtx *cp = host_ctx();
   if (!cp) return VDS_EC_ENODEV;
   HostCtx &c = *cp;
-  // replicas, then n + 1 digests at a 16-byte aligned offset: one push out
+  // replicas, then n digests at a 16-byte aligned offset: one push out
   const uint64_t dig = (L * n + 15) & ~15ull;
-  rc = c.ensure(size ? size : 1, dig + 32ull * (n + 1));
+  rc = c.ensure(size ? size : 1, dig + 32ull * (n ? n : 1));
   if (!rc) rc = c.stage_in(data, size);
   if (rc) return rc;
-  // upload_data's hash of the body (server_api.cpp:16)
-  hipError_t e = launch_sha256(c.d_in, size, size, 1, c.d_out + dig + 32ull * n, c.stream);
-  if (e != hipSuccess) return hip_status(e);
   std::vector<Copy> parts;
   if (n) {
     std::vector<uint16_t> ids(n);
@@ -3161,13 +3158,20 @@ int vds_ec_save_temp16_host(uint16_t k, uint32_t n, const uint8_t *data, uint64_
     }
     rc = encode_device(2, k, ids.data(), n, c.d_in, size, size, 1, douts.data(), 0, 0, c.stream);
     if (rc) return rc;
-    e = launch_sha256(c.d_out, L, L, n, c.d_out + dig, c.stream);  // save_temp's replica names (:79)
+    hipError_t e = launch_sha256(c.d_out, L, L, n, c.d_out + dig, c.stream);  // save_temp's replica names (:79)
+    if (e != hipSuccess) return hip_status(e);
+    e = launch_push(c.h_out_dev, c.d_out, dig + 32ull * n, c.stream);
     if (e != hipSuccess) return hip_status(e);
     parts.push_back({replica_digests, c.h_out + dig, 32ull * n});
   }
-  if ((rc = c.push_out_and_wait(dig + 32ull * (n + 1)))) return rc;
-  parts.push_back({data_digest, c.h_out + dig + 32ull * n, 32});
-  parallel_copy(parts);
+  // upload_data's hash of the body (server_api.cpp:16) on this thread while
+  // the device works: one sequential chain, ~3 us a block in a GPU lane
+  // (sha256_host.cpp)
+  sha256_host(data, size, data_digest);
+  if (n) {
+    if ((rc = hip_status(hipStreamSynchronize(c.stream)))) return rc;
+    parallel_copy(parts);
+  }
   return VDS_EC_OK;
 }
 

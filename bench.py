@@ -245,10 +245,14 @@ def save_temp_leg(torch, chunk, dev, stream, inp, objects, size, k, n, L, Ls, ti
     assert all(hashlib.sha256(hb[i * Ls:i * Ls + L]).digest() == dg[32 * i:32 * (i + 1)] for i in range(2 * n)), \
         "save_temp sha"
     del rep, dig
-    return {"save_temp_GiBps": gib(objects * size, pip_gpu), "serial_GiBps": gib(objects * size, ser_gpu),
+    pip, ser = gib(objects * size, pip_gpu), gib(objects * size, ser_gpu)
+    # headline: the faster schedule, named (both kernels are VALU-heavy, so
+    # the two-stream pipeline has measured slower than serial: DESIGN.md 9.3)
+    return {"save_temp_GiBps": max(pip, ser), "save_temp_schedule": "pipelined" if pip >= ser else "serial",
+            "pipelined_GiBps": pip, "serial_GiBps": ser,
             "batches": batches, "layout": "replicas object-major [objects][n][Ls]",
-            "what": "encode of replicas 0..n-1 + SHA-256 of each, batch b's hashes on a second stream "
-                    "beside batch b+1's encode"}
+            "what": "encode of replicas 0..n-1 + SHA-256 of each; pipelined: batch b's hashes on a second stream "
+                    "beside batch b+1's encode; serial: one stream"}
 
 
 def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02, 0.25), seed=1, align=256):
@@ -307,14 +311,29 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02
         chunk.sha256_device(reps, L, Ls, n * objects, digests, stream)
 
     gib = lambda nbytes, t: round(nbytes / t / 2**30, 3) if t else None
+
+    def roof(nbytes, t, what):
+        """Per-leg roofline: algorithmic HBM bytes of one call (SURVEY.md 8(d):
+        encode S + n L, restore k L + S, regenerate k L + L per object; SHA-256
+        L read + 32 written per message) over the call's device time (HIP
+        events around the call on its stream: every kernel and copy of it)."""
+        if not t:
+            return None
+        return {"algorithmic_bytes_per_call": int(nbytes), "gpu_ms_per_call": round(t * 1e3, 4),
+                "achieved_GBps": round(nbytes / t / 1e9, 1), "peak_GBps": HBM_PEAK_GBPS,
+                "frac": round(nbytes / t / 1e9 / HBM_PEAK_GBPS, 4), "bytes": what}
+
     with torch.cuda.stream(stream):
         enc_wall, enc_gpu = timed(enc)
         sha_wall, sha_gpu = timed(sha)
     torch.cuda.synchronize(dev)
+    enc_bytes, sha_bytes = objects * (size + n * L), n * objects * (L + 32)
     res = {"shape": f"k={k}, n={n}, {objects} x 64 KiB objects, replica stride {Ls} B",
            "encode_GiBps": gib(objects * size, enc_gpu),
            "sha256_replicas_GiBps": gib(n * objects * L, sha_gpu),
-           "sha256_object_GiBps": gib(objects * size, sha_gpu)}
+           "sha256_object_GiBps": gib(objects * size, sha_gpu),
+           "roofline": {"encode": roof(enc_bytes, enc_gpu, "objects x (S + n L)"),
+                        "sha256": roof(sha_bytes, sha_gpu, "n objects x (L + 32)")}}
     # spot-check the digests against hashlib
     import hashlib
     hb = reps.view(-1)[: 4 * Ls].cpu().numpy().tobytes()
@@ -368,6 +387,8 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02
             assert torch.equal(rg_out.view(-1, Ls)[:len(rg), :L], want), f"live regenerate differs (p={loss})"
         syn_pts = int(((nodes < 40).all(axis=1)).sum())
         leg = {"loss": loss, "restorable": int(len(objs)), "regenerated": int(len(rg)),
+               "roofline": {"repair": roof(len(objs) * (k * L + size), rest_gpu, "restorable x (k L + S)"),
+                            "regenerate": roof(len(rg) * (k * L + L), regen_gpu, "regenerated x (k L + L)")},
                "repair_GiBps": gib(len(objs) * size, rest_gpu),
                "repair_host_GiBps": gib(len(objs) * size, rest_wall),
                "regenerate_GiBps": gib(len(rg) * size, regen_gpu),

@@ -30,10 +30,11 @@ LOCK = os.path.join(HERE, ".build.lock")
 # one translation unit per kernel family, compiled in parallel
 SOURCES = ["ec_encode_16_20.hip", "ec_encode_32_40.hip", "ec_encode_32_64.hip", "ec_restore_syn_32a.hip",
            "ec_restore_syn_32b.hip", "ec_restore_syn_16.hip", "ec_encode.hip", "ec_restore_syn.hip", "ec_generic.hip",
-           "ec_restore_bs.hip", "sha256.hip", "vds_ec_api.cpp", "vds_ec_wire.cpp", "vds_ec_jit.cpp", "sha256_host.cpp"]
+           "ec_restore_bs.hip", "sha256.hip", "vds_ec_api.cpp", "api_batch.cpp", "api_host_batch.cpp", "api_param_ring.cpp",
+           "vds_ec_wire.cpp", "vds_ec_jit.cpp", "sha256_host.cpp"]
 HOST_ONLY = {"sha256_host.cpp"}
 HEADERS = ["bitslice.hpp", "gf_common.hpp", "ec_internal.hpp", "ec_device.hpp", "restore_syn.hpp", "xorprog.hpp",
-           "ec_encode.hpp", "ec_restore_syn.hpp", "vds_ec_jitc.cpp"]
+           "ec_encode.hpp", "ec_restore_syn.hpp", "api_internal.hpp", "vds_ec_jitc.cpp"]
 # The device sources the run-time kernels are compiled from (vds_ec_jit.cpp,
 # hiprtc in the helper vds_ec_jitc), embedded in the helper as jit_embed.inc
 # (written into the build directory).

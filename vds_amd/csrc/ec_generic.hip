@@ -377,15 +377,24 @@ __global__ void k_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count) 
 static std::mutex g_tables_mu;
 static uint64_t g_tables_ready = 0;  // bit d: device d has the log / exp tables (g_tables_mu)
 
-static hipError_t ensure_gf16_tables(hipStream_t s) {
+// Built once per device on a private stream, which this thread then waits
+// for: the caller's stream is neither synchronised nor used, so a
+// stream-ordered *_device call that gets here first still only enqueues on
+// it (and works under stream capture); every later launch on any stream sees
+// the finished tables.
+static hipError_t ensure_gf16_tables() {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> g(g_tables_mu);
   if (dev < 64 && ((g_tables_ready >> dev) & 1u)) return hipSuccess;
-  hipLaunchKernelGGL(k_gf16_tables, dim3((65535 + 255) / 256), dim3(256), 0, s);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;  // (once per device: every later stream sees them)
+  hipStream_t own = nullptr;
+  if ((e = hipStreamCreateWithFlags(&own, hipStreamNonBlocking)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gf16_tables, dim3((65535 + 255) / 256), dim3(256), 0, own);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(own);
+  (void)hipStreamDestroy(own);
+  if (e != hipSuccess) return e;
   if (dev < 64) g_tables_ready |= 1ull << dev;
   return hipSuccess;
 }
@@ -497,7 +506,7 @@ hipError_t launch_regen_tail_rt(uint32_t k, const SynBatchObj *objs, uint32_t co
 hipError_t launch_rt_coefs(uint32_t k, const SynBatchObj *objs, uint32_t count, hipStream_t s) {
   if (count == 0) return hipSuccess;
   if (k > 64) return hipErrorInvalidValue;
-  const hipError_t te = ensure_gf16_tables(s);
+  const hipError_t te = ensure_gf16_tables();
   if (te != hipSuccess) return te;
   const uint32_t waves = 4, grid = (count + waves - 1) / waves < 8192u ? (count + waves - 1) / waves : 8192u;
   hipLaunchKernelGGL(k_rt_coefs, dim3(grid), dim3(64 * waves), 0, s, k, objs, count);

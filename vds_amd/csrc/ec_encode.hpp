@@ -18,6 +18,10 @@
 
 namespace vds_ec {
 
+#ifndef VDS_ENC_PLAN_LS
+#define VDS_ENC_PLAN_LS 1  // local search after the LPT pair plan (plan_pairs)
+#endif
+
 // VALU cost of one row-form Horner step for replica r (bitslice.hpp): used
 // to balance replicas across waves.
 constexpr int horner_cost(int r) { return r == 0 ? 1 : row_horner_cost((uint32_t)r); }
@@ -99,7 +103,11 @@ constexpr PairPlan<WAVES, PPW> plan_pairs() {
   int cnt[WAVES] = {};
   bool used[N / 2 + 1] = {};
   int cost[N / 2 + 1] = {};
-  for (int q = 0; q < N / 2; ++q) cost[q] = pair_cost(2 * q);  // (once each: constexpr step limit)
+  // per cell step: the pair's two half-Horner steps, plus its two replica
+  // stores (two 16x16 transposes and 16 dword stores each, ~100 VALU) spread
+  // over the K / 2 = 2 WAVES steps
+  constexpr int kStoreUnits = VDS_ENC_PLAN_LS ? (2 * 100 + WAVES) / (2 * WAVES) : 0;
+  for (int q = 0; q < N / 2; ++q) cost[q] = pair_cost(2 * q) + kStoreUnits;  // (once each: constexpr step limit)
   for (int w = 0; w < WAVES; ++w)
     for (int s = 0; s < PPW; ++s) p.r[w][s] = -1;
   for (int it = 0; it < N / 2; ++it) {
@@ -112,6 +120,48 @@ constexpr PairPlan<WAVES, PPW> plan_pairs() {
       if (cnt[w] < PPW && (bw < 0 || load[w] < load[bw])) bw = w;
     p.r[bw][cnt[bw]++] = 2 * best;
     load[bw] += cost[best];
+  }
+  // Then local search on the largest load (VDS_ENC_PLAN_LS): move one pair of
+  // the most loaded wave to a wave with room, or swap it with a pair of
+  // another wave, whenever that lowers the larger of the two loads.  LPT left
+  // 20 pairs on 8 waves at loads 162..205 (k = 32, n = 40) and 10 on 4 at
+  // 130..171 (k = 16): a wave that runs alone once its SIMD partner is done
+  // issues at about half the rate, so the tile waits on the heaviest wave.
+  if constexpr (VDS_ENC_PLAN_LS) {
+    for (int round = 0; round < 64; ++round) {
+      int a = 0;
+      for (int w = 1; w < WAVES; ++w)
+        if (load[w] > load[a]) a = w;
+      int gain = 0, bi = -1, bw = -1, bj = -1;  // best: item bi of a -> wave bw (bj = -1) or swap with item bj of bw
+      for (int i = 0; i < cnt[a]; ++i) {
+        const int ci = cost[p.r[a][i] / 2];
+        for (int w = 0; w < WAVES; ++w) {
+          if (w == a) continue;
+          if (cnt[w] < PPW) {  // move
+            const int m = (load[a] - ci > load[w] + ci) ? load[a] - ci : load[w] + ci;
+            if (load[a] - m > gain) gain = load[a] - m, bi = i, bw = w, bj = -1;
+          }
+          for (int j = 0; j < cnt[w]; ++j) {  // swap
+            const int cj = cost[p.r[w][j] / 2];
+            const int la = load[a] - ci + cj, lw = load[w] - cj + ci;
+            const int m = la > lw ? la : lw;
+            if (load[a] - m > gain) gain = load[a] - m, bi = i, bw = w, bj = j;
+          }
+        }
+      }
+      if (bi < 0) break;
+      const int ri = p.r[a][bi], ci = cost[ri / 2];
+      if (bj < 0) {
+        p.r[a][bi] = p.r[a][--cnt[a]];
+        p.r[a][cnt[a]] = -1;
+        p.r[bw][cnt[bw]++] = ri;
+        load[a] -= ci, load[bw] += ci;
+      } else {
+        const int rj = p.r[bw][bj], cj = cost[rj / 2];
+        p.r[a][bi] = rj, p.r[bw][bj] = ri;
+        load[a] += cj - ci, load[bw] += ci - cj;
+      }
+    }
   }
   return p;
 }

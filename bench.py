@@ -396,7 +396,8 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02
                "distinct_survivor_sets": int(len({tuple(r) for r in nodes.tolist()})),
                "survivors_within_0_39": syn_pts}
         if loss == losses[0]:  # (the round-2 keys: the first loss rate)
-            res.update({kk: v for kk, v in leg.items() if kk not in ("loss",)})
+            res.update({kk: v for kk, v in leg.items() if kk not in ("loss", "roofline")})
+            res["roofline"].update(leg["roofline"])
             res["shape"] += f"; replica loss p={loss}; {len(objs)} restorable, {len(rg)} regenerated"
         res[f"loss_{loss}"] = leg
         del rg_out

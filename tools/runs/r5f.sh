@@ -1,9 +1,7 @@
-# Round 5: checkpoint (GPU suite, default bench, latency), then two A/Bs at
-# the same box, interleaved: the encode pair plan (ab/nols: LPT only) at k = 16
+# Round 5: two A/Bs on one box, interleaved (run tools/runs/r5_check.sh first): the encode pair plan (ab/nols: LPT only) at k = 16
 # (512 objects) and k = 32 (256); the k = 32 restore's LDS-DMA prefetch
 # (ab/nodma: VDS_K32_DMA=0) at 256 objects.
 cd $GRAFT_REPO_ROOT
-bash tools/runs/r5_check.sh r5chk1 || exit $?
 row() { python - "$@" <<'PY'
 import json, sys
 out = [sys.argv[1]]

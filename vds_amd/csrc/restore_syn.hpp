@@ -257,35 +257,6 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
 #ifndef VDS_HALF_PRIO
 #define VDS_HALF_PRIO 1
 #endif
-// k = 32, N = 40, one object per launch (C4): slots 32..39 are free from the
-// end of phase 2 to the next tile's stage 1, so waves 1..7 bring their fourth
-// survivor of the next tile into slot 32 + w by LDS-DMA right after phase 2
-// (global_load_lds_dwordx4: no VGPRs) instead of with the late loads after
-// the interpolation.  Slot 32 itself is left alone: the copy-out staging
-// reaches 2 KiB into it.  The DMA is issued from inline asm, so the compiler
-// does not know an LDS write is in flight: it would otherwise wait vmcnt(0)
-// at every later LDS access and barrier (it cannot prove they do not alias),
-// draining the DMA -- and the previous tile's stores -- at once.  Stage 1
-// waits for it with a counted vmcnt (the 16 copy-out stores, younger, stay
-// in flight), reads it into registers, and only after a barrier does any
-// wave write slots >= 32 again.
-#ifndef VDS_K32_DMA
-#define VDS_K32_DMA 1
-#endif
-// 16 bytes per lane of `src` (a global address) to LDS byte `lds` + 16 lane
-__device__ __forceinline__ void lds_dma16(const uint8_t *src, uint32_t lds) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n"
-      "s_mov_b32 m0, %2\n"
-      "s_nop 0\n"
-      "global_load_lds_dwordx4 %1, off\n"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds)
-      : "memory");
-}
-
 template <int K, int N, int WV, int W>
 __device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
   using P = RestorePrograms<K, N, WV>;
@@ -572,7 +543,6 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   constexpr bool kSmall = FillP::kSmall;
   constexpr bool kPerm = FillP::kPerm;
   constexpr bool kMulti = FillP::kMulti;
-  constexpr bool kDma = VDS_K32_DMA && K == 32 && N == 40 && !BATCH && !REGEN && !RT;
   static_assert(!kMulti || (BATCH && !RT), "MULTI is a batch mode");
   static_assert(!kSmall || (BATCH && !RT && !FILL), "SMALL is a batch mode of its own");
   static_assert(!kPerm || (BATCH && REGEN && !RT && !FILL), "PERM is a batch regenerate mode of its own");
@@ -636,11 +606,6 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       const uint64_t st0 = stripe0_of(t);
 #pragma unroll
       for (int s = 0; s < S::kLoadPer; ++s) {
-        if (kDma && s == 3 && wave > 0) {  // (LDS-DMA: dma_issue; defined here so the old value dies at stage 1)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) Q[s][q] = u32x4{0u, 0u, 0u, 0u};
-          continue;
-        }
         const uint8_t *src = a.chunks[wave * S::kLoadPer + s] + (uint64_t)ob * a.chunk_stride + 2 * st0 + 16 * lane;
 #pragma unroll
         for (int q = 0; q < 4; ++q) Q[s][q] = g_ld<4, u32x4>(src + 1024 * q);
@@ -676,19 +641,6 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   // 90 VGPRs spilled, round 5 tools/jit_dump.py)
   constexpr bool kLateLoad = ((K == 32 || BATCH) && !REGEN) || RT;
   const uint32_t t_step = tr.step;
-  // the fourth survivor of waves 1..7 by LDS-DMA into slot 32 + wave (VDS_K32_DMA)
-  auto dma_issue = [&](uint32_t t) {
-    if constexpr (kDma) {
-      if (wave > 0 && t < tr.end) {
-        const uint8_t *src = a.chunks[wave * S::kLoadPer + 3] + (uint64_t)obj_of(t) * a.chunk_stride +
-                             2 * stripe0_of(t) + 16 * lane;
-        const uint32_t dst = (uint32_t)(uintptr_t)(L.base + 4096u * (32 + wave));  // (wave-uniform)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) lds_dma16(src + 1024 * q, __builtin_amdgcn_readfirstlane(dst + 1024u * q));
-      }
-    }
-  };
-  dma_issue(tr.first);  // (issued before the loads: stage 1's counted wait covers it)
   prefetch(tr.first);
   // vmcnt counts loads and stores together and retires them in issue order.
   // In the loop, the 16 copy-out stores of a tile are issued after the next
@@ -725,18 +677,6 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     // PERM evaluations of P0 and |E| x |E| runtime products
     constexpr bool kRt2 = RT && !REGEN && K == 32 && N >= K + 8;
     const bool rt2_tile = kRt2 && s_ld(&a.tiles[tile].mode) == 1u;
-    if constexpr (kDma) {
-      // the DMA'd fourth survivor: every VMEM op but this tile's 16 copy-out
-      // stores... of the previous tile (the youngest) is done, then into the
-      // registers; no wave writes slots >= 32 before every wave has read its own
-      if (wave > 0) {
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        const lds_char *r = L.base + 4096u * (32 + wave) + 16u * lane;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) Q[3][q] = *(const lds_v4 *)(r + 1024 * q);
-      }
-      __syncthreads();
-    }
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
     syn_prio<1, kPrio>();
     uint64_t bor[2] = {0, 0};  // RT restore: borrowed slots of each half
@@ -1185,7 +1125,6 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     st.mark(5);
     __syncthreads();
     st.mark(6);
-    dma_issue(tile + t_step);  // (kDma: slots 32..39 are free until the next tile's stage 1)
     if constexpr (REGEN) {
       // ---- 3'. regenerate: the recovered point e_w IS replica e_w's cells
       // (P(e_w) stripe by stripe).  Undo the stage-1 transpose and store it as

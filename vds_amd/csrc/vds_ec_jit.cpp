@@ -55,9 +55,6 @@ extern char **environ;
 #ifndef VDS_HALF_PRIO
 #define VDS_HALF_PRIO 1
 #endif
-#ifndef VDS_K32_DMA
-#define VDS_K32_DMA 1
-#endif
 #ifndef VDS_DIAG_STAMPS
 #define VDS_DIAG_STAMPS 0
 #endif
@@ -154,8 +151,8 @@ std::string kernel_source(const Key &key) {
     if ((key.survivors >> a) & 1u) sp.push_back(a);
   std::string s;
   xorgen::appendf(s,
-                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n#define VDS_HALF_PRIO %d\n#define VDS_K32_DMA %d\n",
-                  VDS_GM2, VDS_GM2_PRIO, VDS_HALF_PRIO, VDS_K32_DMA);  // (the forms this library was built with)
+                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n#define VDS_HALF_PRIO %d\n", VDS_GM2,
+                  VDS_GM2_PRIO, VDS_HALF_PRIO);  // (the forms this library was built with)
 #if VDS_DIAG_STAMPS
   xorgen::appendf(s, "#define VDS_DIAG_STAMPS 1\n");  // (phase stamps: vds_ec_diag_jit_stamps)
 #endif

@@ -62,7 +62,8 @@ static size_t emit_program(const char *name, const std::vector<std::vector<int>>
 //      slots 4W..4W+3 (j = W, i = 2W, 2W+1).
 //   S2: family f (slots 4j + f: f = par for R0 of Q_par, par + 2 for R1) is
 //      interpolated directly on its K/4 points s(ptR(2j)); coefficient c ->
-//      slot 4c + f.  K = 16: one wave per family, in place; K = 32: two.
+//      slot 4c + f.  K = 16: one wave per family, in place; K = 32: two, each
+//      computing half the bit planes of every coefficient.
 //   S3: Q_par coefficient i = delta^-i (sum_c [C(c, i-c) odd] R0_c + [C(c,
 //      i-1-c) odd] R1_c) (the expansion R(Y) = R0(Y^2+Y) + Y R1(Y^2+Y), then
 //      the twist) -> slot (K/2) par + i: the layout stage C reads.
@@ -148,8 +149,18 @@ static size_t emit_gm2(int K, int waves) {
     xorgen::InputMap im;
     for (int j = 0; j < F; ++j) im.map.push_back(4 * j + f);
     std::vector<int> rowsel;
-    for (int c = c0; c < c0 + 4; ++c)
-      for (int b = 0; b < 16; ++b) rowsel.push_back(16 * c + b);
+    if (wpf == 1) {  // K = 16: the wave's family whole
+      for (int c = c0; c < c0 + 4; ++c)
+        for (int b = 0; b < 16; ++b) rowsel.push_back(16 * c + b);
+    } else {
+      // K = 32: the two waves of a family split the planes (h = w % 2: planes
+      // 8h..8h+7 of all 8 coefficients, acc[8c + b - 8h]); split by
+      // coefficients instead, the halves' programs cost 889 and 1069 XORs
+      // (every 4 + 4 split: at least 1060), split by planes 999 and 994
+      const int h = w % wpf;
+      for (int c = 0; c < F; ++c)
+        for (int b = 8 * h; b < 8 * h + 8; ++b) rowsel.push_back(16 * c + b);
+    }
     char name[32];
     std::snprintf(name, sizeof name, "gm_s2_%d", w);
     std::string s;

@@ -276,12 +276,25 @@ __device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, uint32
     __syncthreads();
     st.mark(8);
     // S2: family f = W / kWpf (slots 4j + f), coefficients c0.. -> slot 4c + f
+    // (k = 32: the family's two waves each hold planes 8h..8h+7 of all eight
+    // coefficients, acc[8c + ..], h = W % 2: gen_restore.cpp emit_gm2)
     syn_prio<1, kPrio && (VDS_GM2_PRIO & 2)>();
     P::gm_s2_(W, L, acc);
     constexpr int f = W / kWpf, c0 = 4 * (W % kWpf);
-    if constexpr (kWpf > 1) __syncthreads();  // (every wave of the family has read it)
+    if constexpr (kWpf > 1) {
+      __syncthreads();  // (every wave of the family has read it)
+      constexpr int h = W % kWpf;
+      static_assert(kWpf == 2 && K / 4 == 8, "plane-split S2 is laid out for k = 32");
 #pragma unroll
-    for (int c = 0; c < 4; ++c) syn_put_point(L, 4 * (c0 + c) + f, cell(c));
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+          L.put(4 * (4 * c + f) + 2 * h + g,
+                u32x4{acc[8 * c + 4 * g], acc[8 * c + 4 * g + 1], acc[8 * c + 4 * g + 2], acc[8 * c + 4 * g + 3]});
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) syn_put_point(L, 4 * (c0 + c) + f, cell(c));
+    }
     syn_prio<0, kPrio && (VDS_GM2_PRIO & 2)>();
     st.mark(9);
     __syncthreads();

@@ -17,7 +17,8 @@ import sys
 
 
 def main() -> int:
-    bench = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+    lines = [l for l in open(sys.argv[1]).read().splitlines() if l.startswith('{"metric"')]
+    bench = json.loads(lines[-1])  # (rocprofv3 prints after the bench line)
     stats = {}
     for r in csv.DictReader(open(sys.argv[2])):
         stats[r["Name"]] = (float(r["AverageNs"]) * 1e-6, int(r["Calls"]))

@@ -167,27 +167,49 @@ __device__ __forceinline__ void syn_gm_stage_a(const SynLds &L) {
 // Output cell k = sum of P0_i with C(i, k - i) odd and of P1_i with
 // C(i, k - 1 - i) odd (Lucas: C(i, m) is odd iff the bits of m are a subset of
 // those of i).  P0_i sits in LDS slot i, P1_i in slot K/2 + i.
-template <int K, int W, int NC>
+// k = 16: each slot the wave's cells use is read once and XORed into every
+// cell that takes it (slot-major).  Cell-major (G = 1), the compiler re-read
+// a slot for every cell that takes it: 54 slot reads per tile for 30 distinct
+// ones (wave 3: 36 ds_read_b128 for 4 slots).  Same box, three interleaved
+// rounds at 512 x 64 MiB (profiles/round5/ab_stagec.log): survivor-set repair
+// 14.22-14.38 -> 14.15-14.26 ms, k_restore_syn<16,20> 16.78-16.86 -> 16.55-
+// 16.60.  k = 32 keeps cell-major: all four cells at once spilled 96 VGPRs
+// beside the late loads, two at a time (162 -> 122 slot reads) measured
+// 10.13-10.19 -> 10.19-10.25 ms (256 x 64 MiB).
+template <int K, int W, int NC, int G = (K == 16 ? NC : 1)>
 __device__ __forceinline__ void syn_gm_stage_c(const SynLds &L, uint32_t (&cells)[16 * NC]) {
+  constexpr auto takes = [](int c, int t) {
+    const int k = NC * W + c, i = t % (K / 2);
+    const int m = t < K / 2 ? k - i : k - 1 - i;
+    return m >= 0 && m <= i && (m & ~i) == 0;
+  };
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int k = NC * W + c;
-    uint32_t acc[16];
+  for (int c0 = 0; c0 < NC; c0 += G) {
+    bool first[G];
 #pragma unroll
-    for (int b = 0; b < 16; ++b) acc[b] = 0u;
+    for (int c = 0; c < G; ++c) first[c] = true;
 #pragma unroll
     for (int t = 0; t < K; ++t) {
-      const int i = t % (K / 2);
-      const int m = t < K / 2 ? k - i : k - 1 - i;
-      if (m >= 0 && m <= i && (m & ~i) == 0) {
+      bool any = false;
+#pragma unroll
+      for (int c = 0; c < G; ++c) any |= takes(c0 + c, t);
+      if (any) {
         uint32_t v[16];
         syn_get_point(L, t, v);
 #pragma unroll
-        for (int b = 0; b < 16; ++b) acc[b] ^= v[b];
+        for (int c = 0; c < G; ++c)
+          if (takes(c0 + c, t)) {
+#pragma unroll
+            for (int b = 0; b < 16; ++b) cells[16 * (c0 + c) + b] = first[c] ? v[b] : cells[16 * (c0 + c) + b] ^ v[b];
+            first[c] = false;
+          }
       }
     }
 #pragma unroll
-    for (int b = 0; b < 16; ++b) cells[16 * c + b] = acc[b];
+    for (int c = 0; c < G; ++c)
+      if (first[c])
+#pragma unroll
+        for (int b = 0; b < 16; ++b) cells[16 * (c0 + c) + b] = 0u;
   }
 }
 
@@ -549,6 +571,9 @@ template <int K> struct PermSyn;
 // all.  Against the N = K + K/4 syndrome kernel at MS = 2: 2.4K instead of
 // 13.4K syndrome XORs per tile (k = 32), and no M x M runtime walk.
 template <int K, int MS> struct SmallSyn;
+#ifndef VDS_SYN_RT2
+#define VDS_SYN_RT2 1  // (A/B: 0 compiles the RT kernels without the RT2 rows)
+#endif
 template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false, class FillP = NoFill>
 __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   constexpr bool FILL = FillP::kFill >= 0;
@@ -688,7 +713,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     Plane16 Ps[RT ? S::kLoadPer : 1];  // RT: this wave's slots, kept for phase 2
     // RT2 tile (SynBatchRt, ec_internal.hpp): restore at k = 32 through the
     // PERM evaluations of P0 and |E| x |E| runtime products
-    constexpr bool kRt2 = RT && !REGEN && K == 32 && N >= K + 8;
+    constexpr bool kRt2 = VDS_SYN_RT2 && RT && !REGEN && K == 32 && N >= K + 8;
     const bool rt2_tile = kRt2 && s_ld(&a.tiles[tile].mode) == 1u;
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
     syn_prio<1, kPrio>();

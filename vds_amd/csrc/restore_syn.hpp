@@ -279,13 +279,14 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
 #ifndef VDS_HALF_PRIO
 #define VDS_HALF_PRIO 1
 #endif
-template <int K, int N, int WV, int W>
-__device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, uint32_t (&cells)[16 * (K / WV)], Stamps &st) {
+template <int K, int N, int WV, int W, class Tail>
+__device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, Stamps &st, Tail &&tail) {
   using P = RestorePrograms<K, N, WV>;
   constexpr bool kPrio = SynShape<K, N, WV>::kPrio;
   constexpr int H = K / 2, kWpf = WV / 4, kWpq = WV / 2;
   if constexpr (W < WV) {
-    if (wave != W) return syn_interp_gm2<K, N, WV, W + 1>(wave, L, cells, st);
+    if (wave != W) return syn_interp_gm2<K, N, WV, W + 1>(wave, L, st, tail);
+    uint32_t cells[16 * (K / WV)];
     uint32_t acc[64];
     auto cell = [&](int c) -> uint32_t(&)[16] { return *reinterpret_cast<uint32_t(*)[16]>(acc + 16 * c); };
     // S1: levels 1 and 2 on this wave's slots 4W..4W+3 (only this wave touches them)
@@ -338,6 +339,7 @@ __device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, uint32
     syn_gm_stage_c<K, W, K / WV>(L, cells);
     syn_prio<0, kPrio && (VDS_GM2_PRIO & 8)>();
     st.mark(13);
+    tail(cells);  // (staging and copy-out, in this wave's branch: see the caller)
   }
 }
 
@@ -1227,11 +1229,15 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     }
     // ---- 3. fixed interpolation from points 0..K-1, then big-endian stores
     {
-      uint32_t cells[16 * S::kCells];
-      if constexpr (VDS_GM2 != 0)
-        syn_interp_gm2<K, N, WV, 0>(wave, L, cells, st);
-      else
-        syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
+      // RT kernels run the staging and copy-out (the tail) inside each wave's
+      // interpolation branch: after the join of the WV branches the cells
+      // are a merge of WV definitions, and the k = 32 RT kernel (RT2 rows
+      // compiled in) spilled 22 of them per wave to scratch at every tile
+      // (176 VGPRs; 24 with the tail in the branches).  The other kernels
+      // keep the join: with the tail in the branches the plain k = 32 kernel
+      // spilled 1,844 (the late loads beside the staging).
+      constexpr bool kTailInWave = RT;
+      auto tail = [&](uint32_t (&cells)[16 * S::kCells]) {
       if (kLateLoad && !BATCH) prefetch(tile + t_step);
       // this wave's copy-out: 1024 kChunks bytes at wofs of the tile's output
       // (batch: of its half's object's output, with out_valid bytes of the
@@ -1373,6 +1379,21 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
           for (int i = 0; i < 16; ++i) st16_guard(g0 + 1024 * i, piece(i), out_valid - 16 * lane - 1024 * i);
         }
         st.mark(17);
+      }
+      };
+      if constexpr (VDS_GM2 != 0 && kTailInWave) {
+        syn_interp_gm2<K, N, WV, 0>(wave, L, st, tail);
+      } else if constexpr (VDS_GM2 != 0) {
+        uint32_t cells[16 * S::kCells];
+        syn_interp_gm2<K, N, WV, 0>(wave, L, st, [&](uint32_t (&c)[16 * S::kCells]) {
+#pragma unroll
+          for (int i = 0; i < 16 * S::kCells; ++i) cells[i] = c[i];
+        });
+        tail(cells);
+      } else {
+        uint32_t cells[16 * S::kCells];
+        syn_interp_gm<K, N, WV, 0>(wave, L, cells, st);
+        tail(cells);
       }
     }
     __syncthreads();

@@ -462,14 +462,41 @@ __device__ __forceinline__ void lds_xor_point(const SynLds &L, int pt, const Pla
 // erased point below K, XORed into the zeroed slots.  Dispatched on a
 // compile-time wave so each arm stores its own results (a runtime switch
 // merged the 64 result registers of all arms and spilled them).
-template <int WV, class FillP, int W>
-__device__ __forceinline__ void syn_scatter_fill(int wave, const SynLds &L) {
+// VDS_FILL_REGS (k = 16): the programs read the wave's four survivors from
+// the stage-1 registers (FillRegIn) instead of reading back the slots it has
+// just stored (16 of the tile's ~920 LDS instructions per wave).  Same box,
+// three interleaved rounds at 512 x 64 MiB, with the staging in each wave's
+// branch (below): survivor-set repair 14.08-14.36 -> 13.87-13.99 ms
+// (profiles/round5/ab_fill_regs.log).  Running the fill's XORs before stage
+// 1's barrier as well (one barrier in each wave's arm, guarding only the
+// atomics) measured no better than before: 14.04-14.16 ms.
+#ifndef VDS_FILL_REGS
+#define VDS_FILL_REGS 1
+#endif
+template <class FillP, int W>
+struct FillRegIn {
+  const Plane16 (&P)[4];
+  static constexpr int slot(int pt) {
+    for (int i = 0; i < 4; ++i)
+      if (FillP::kSurv[4 * W + i] == pt) return i;
+    return -1;
+  }
+  __device__ __forceinline__ u32x4 operator()(int idx) const {
+    const int i = slot(idx >> 2), g = idx & 3;
+    return u32x4{P[i].p[4 * g], P[i].p[4 * g + 1], P[i].p[4 * g + 2], P[i].p[4 * g + 3]};
+  }
+};
+template <int WV, class FillP, bool REGS, int W>
+__device__ __forceinline__ void syn_scatter_fill(int wave, const SynLds &L, const Plane16 (&Ps)[4]) {
   if constexpr (W < WV) {
-    if (wave != W) return syn_scatter_fill<WV, FillP, W + 1>(wave, L);
+    if (wave != W) return syn_scatter_fill<WV, FillP, REGS, W + 1>(wave, L, Ps);
 #pragma unroll
     for (int q = 0; q < FillP::kParts; ++q) {
       uint32_t acc[16 * FillP::kPart];
-      FillP::fill_part(q, W, L, acc);
+      if constexpr (REGS)
+        FillP::fill_part(q, W, FillRegIn<FillP, W>{Ps}, acc);
+      else
+        FillP::fill_part(q, W, L, acc);
 #pragma unroll
       for (int m = 0; m < FillP::kPart; ++m)
         if (q * FillP::kPart + m < FillP::kFill)
@@ -712,7 +739,12 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     const uint32_t cls = kMulti ? s_ld(&pl->cls) : (kPerm ? kClsPerm : kClsSyn);
     const bool perm_tile = kPerm || (kMulti && REGEN && cls == kClsPerm);
     const int my_erased = RT ? K + wave : perm_tile ? K : (wave < S::kM ? erased_of(wave) : 0);
-    Plane16 Ps[RT ? S::kLoadPer : 1];  // RT: this wave's slots, kept for phase 2
+    // RT: this wave's slots, kept for phase 2; the scatter fill: its survivors (VDS_FILL_REGS)
+    constexpr bool kFillRegs = kScatter && VDS_FILL_REGS && K == 16;
+    constexpr bool kKeepPs = RT || kFillRegs;
+    static_assert(!kKeepPs || S::kLoadPer == 4, "four survivors per wave");
+    Plane16 Ps[kKeepPs ? S::kLoadPer : 1];
+
     // RT2 tile (SynBatchRt, ec_internal.hpp): restore at k = 32 through the
     // PERM evaluations of P0 and |E| x |E| runtime products
     constexpr bool kRt2 = VDS_SYN_RT2 && RT && !REGEN && K == 32 && N >= K + 8;
@@ -772,6 +804,9 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
             syn_put_point(L, j, Pl);
           }
         } else {
+          if constexpr (kKeepPs)
+#pragma unroll
+            for (int b = 0; b < 16; ++b) Ps[s].p[b] = Pl[b];
           syn_put_point(L, (int)s_ld_u8(BATCH ? pl->point : a.point, wave * S::kLoadPer + s), Pl);
         }
       }
@@ -1136,7 +1171,10 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     } else if constexpr (kScatter) {
       // ---- 2''. this wave's survivors' share of every erased point below K
       // (its own stage-1 slots in, LDS XOR atomics out; survivors sorted by point)
-      syn_scatter_fill<WV, FillP, 0>(wave, L);
+      if constexpr (kFillRegs)
+        syn_scatter_fill<WV, FillP, true, 0>(wave, L, Ps);
+      else
+        syn_scatter_fill<WV, FillP, false, 0>(wave, L, {});
       if (!kLateLoad) prefetch(tile + t_step);
     } else if constexpr (kPerm) {
       phase_perm(TypeTag<FillP>{});
@@ -1229,14 +1267,17 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     }
     // ---- 3. fixed interpolation from points 0..K-1, then big-endian stores
     {
-      // RT kernels run the staging and copy-out (the tail) inside each wave's
-      // interpolation branch: after the join of the WV branches the cells
-      // are a merge of WV definitions, and the k = 32 RT kernel (RT2 rows
-      // compiled in) spilled 22 of them per wave to scratch at every tile
-      // (176 VGPRs; 24 with the tail in the branches).  The other kernels
-      // keep the join: with the tail in the branches the plain k = 32 kernel
-      // spilled 1,844 (the late loads beside the staging).
-      constexpr bool kTailInWave = RT;
+      // The RT kernels and the k = 16 survivor-set kernels run the staging
+      // and copy-out (the tail) inside each wave's interpolation branch:
+      // after the join of the WV branches the cells are a merge of WV
+      // definitions, and the k = 32 RT kernel (RT2 rows compiled in) spilled
+      // 22 of them per wave to scratch at every tile (176 VGPRs; 24 with the
+      // tail in the branches), the k = 16 survivor-set kernel with its fill
+      // from registers 113 (0 in the branches, also without the 5-VGPR zero
+      // vector spill of before).  The other kernels keep the join: with the
+      // tail in the branches the plain k = 32 kernel spilled 1,844 (the late
+      // loads beside the staging).
+      constexpr bool kTailInWave = RT || kFillRegs;
       auto tail = [&](uint32_t (&cells)[16 * S::kCells]) {
       if (kLateLoad && !BATCH) prefetch(tile + t_step);
       // this wave's copy-out: 1024 kChunks bytes at wofs of the tile's output

@@ -55,6 +55,9 @@ extern char **environ;
 #ifndef VDS_HALF_PRIO
 #define VDS_HALF_PRIO 1
 #endif
+#ifndef VDS_FILL_REGS
+#define VDS_FILL_REGS 1
+#endif
 #ifndef VDS_DIAG_STAMPS
 #define VDS_DIAG_STAMPS 0
 #endif
@@ -151,8 +154,9 @@ std::string kernel_source(const Key &key) {
     if ((key.survivors >> a) & 1u) sp.push_back(a);
   std::string s;
   xorgen::appendf(s,
-                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n#define VDS_HALF_PRIO %d\n", VDS_GM2,
-                  VDS_GM2_PRIO, VDS_HALF_PRIO);  // (the forms this library was built with)
+                  "#define VDS_GM2 %d\n#define VDS_GM2_PRIO %d\n#define VDS_HALF_PRIO %d\n"
+                  "#define VDS_FILL_REGS %d\n",
+                  VDS_GM2, VDS_GM2_PRIO, VDS_HALF_PRIO, VDS_FILL_REGS);  // (the forms this library was built with)
 #if VDS_DIAG_STAMPS
   xorgen::appendf(s, "#define VDS_DIAG_STAMPS 1\n");  // (phase stamps: vds_ec_diag_jit_stamps)
 #endif

@@ -414,6 +414,11 @@ inline size_t emit_fill_scatter(std::string &s, const char *name, int K, const s
   appendf(s, "  static constexpr uint8_t kPoint[%d] = {", F ? F : 1);
   for (int e : EU) appendf(s, "%d, ", e);
   appendf(s, "};\n");
+  // the survivors by rank (wave w loaded ranks 4w..4w+3 in stage 1: the
+  // kernel serves IN4 from those registers, restore_syn.hpp FillRegIn)
+  appendf(s, "  static constexpr uint8_t kSurv[%d] = {", K);
+  for (int j = 0; j < K; ++j) appendf(s, "%d, ", spoints[j]);
+  appendf(s, "};\n");
   size_t total = 0;
   for (int w = 0; w < WV; ++w)
     for (int q = 0; q < parts; ++q) {

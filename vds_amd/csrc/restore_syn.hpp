@@ -465,9 +465,9 @@ __device__ __forceinline__ void lds_xor_point(const SynLds &L, int pt, const Pla
 // VDS_FILL_REGS (k = 16): the programs read the wave's four survivors from
 // the stage-1 registers (FillRegIn) instead of reading back the slots it has
 // just stored (16 of the tile's ~920 LDS instructions per wave).  Same box,
-// three interleaved rounds at 512 x 64 MiB, with the staging in each wave's
-// branch (below): survivor-set repair 14.08-14.36 -> 13.87-13.99 ms
-// (profiles/round5/ab_fill_regs.log).  Running the fill's XORs before stage
+// six processes each in ABBA order at 512 x 64 MiB, with the staging in each
+// wave's branch (below): survivor-set repair 14.05-14.18 -> 13.85-13.99 ms,
+// mean -1.3% (profiles/round5/ab_fill_regs_abba.log).  Running the fill's XORs before stage
 // 1's barrier as well (one barrier in each wave's arm, guarding only the
 // atomics) measured no better than before: 14.04-14.16 ms.
 #ifndef VDS_FILL_REGS

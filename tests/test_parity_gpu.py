@@ -687,3 +687,39 @@ def test_c4_full_size_golden(ec, jit):
         assert sha(res.cpu().numpy()) == rest["sha256"]
     finally:
         chunk.jit_set_mode(0)
+
+
+_ORACLE_CACHE = {}
+
+
+@pytest.mark.parametrize("jit", [0, 2], ids=["aot", "jit"])
+def test_headline_full_size_non_codeword_vs_oracle(ec, jit):
+    """The headline configuration (k = 16, n = 20, erased {0, 5, 10, 15}) at
+    full size with survivors that are not one codeword (random bytes): the
+    syndrome kernel k_restore_syn<16,20> (jit 0) and the survivor set's
+    run-time kernel (jit 2: its fill reads the stage-1 registers) against the
+    oracle's restore (chunk.h:402-444).  1024 tiles, so every workgroup walks
+    several of them."""
+    import torch
+    from vds_amd import chunk
+    k, n, size = 16, 20, 64 << 20
+    L = chunk.replica_size(k, size)
+    nodes = [r for r in range(n) if r % 5]
+    if "headline" not in _ORACLE_CACHE:  # (one oracle restore, ~4 s, for both kernels)
+        rng = np.random.default_rng(SEED + 1616)
+        host = [rng.integers(0, 256, L, dtype=np.uint8) for _ in nodes]
+        for c in host:
+            c[-2], c[-1] = 0, 0  # (size % 2k == 0)
+        _ORACLE_CACHE["headline"] = (host, O.restore(k, nodes, host))
+    host, ref = _ORACLE_CACHE["headline"]
+    dev = torch.from_numpy(np.stack(host)).cuda()
+    chunk.jit_set_mode(jit)
+    try:
+        out = torch.zeros(len(ref) + 64, dtype=torch.uint8, device="cuda")
+        chunk.restore_device(k, nodes, [dev[j].data_ptr() for j in range(k)], L, 0, 0, 1, out, 0)
+        torch.cuda.synchronize()
+        assert _path(k, nodes, L) == (4 if jit else 3)
+        assert np.array_equal(out[:len(ref)].cpu().numpy(), ref)
+        assert int(out[len(ref):].sum().item()) == 0
+    finally:
+        chunk.jit_set_mode(0)

@@ -280,20 +280,56 @@ VDS_INLINE uint32_t bit_select(uint32_t m, uint32_t a, uint32_t b) {
 #endif
 }
 
-template <int J, int ROWS, typename Arr>
+VDS_INLINE uint32_t rotl32(uint32_t x, int s) {  // s in 1..31
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(x, x, 32 - s);
+#else
+  return (x << s) | (x >> (32 - s));
+#endif
+}
+
+// The sub-byte rounds J = 4, 2, 1 of a bit transpose, on words kept
+// rotated: each pair (k, k + J) costs one rotate and two selects instead of
+// two shifts and two selects.  Before round J both words of a pair are
+// rotated left by the same r (a multiple of 2J, so the masks, of period 2J,
+// are unchanged); with bs = rotl(b, J),
+//   new_k   = (a & m) | ((b << J) & ~m)  kept rotated by r:     sel(m, a, bs)
+//   new_k+J = ((a >> J) & m) | (b & ~m)  kept rotated by r + J: sel(m, bs, a)
+// (the bits a rotate brings in where a shift brings zeros fall under the
+// other operand's mask).  After rounds 4, 2, 1 word q is rotated by q & 7;
+// rotate_back undoes that.  A transpose16x2 takes 102 instructions instead
+// of 112, a transpose32 236 instead of 256.
+// (ROT = false: the plain shift form, two shifts and two selects per pair;
+// the k = 32 encode keeps it -- 9.45-9.51 vs 9.72-9.78 ms with the rotated
+// one, while the k = 16 repair gained 4%: profiles/round5/ab_transpose.log)
+template <int J, int ROWS, bool ROT, typename Arr>
 VDS_INLINE void transpose_round(Arr &A, const BitMasks &bm) {
   const uint32_t m = (J == 4) ? bm.m4 : (J == 2) ? bm.m2 : bm.m1;
 #pragma unroll
   for (int k0 = 0; k0 < ROWS; k0 += 2 * J)
 #pragma unroll
     for (int k = k0; k < k0 + J; ++k) {
-      const uint32_t a = A[k], b = A[k + J];
-      A[k] = bit_select(m, a, b << J);
-      A[k + J] = bit_select(m, a >> J, b);
+      if constexpr (ROT) {
+        const uint32_t a = A[k], bs = rotl32(A[k + J], J);
+        A[k] = bit_select(m, a, bs);
+        A[k + J] = bit_select(m, bs, a);
+      } else {
+        const uint32_t a = A[k], b = A[k + J];
+        A[k] = bit_select(m, a, b << J);
+        A[k + J] = bit_select(m, a >> J, b);
+      }
     }
+}
+template <int ROWS, bool ROT, typename Arr>
+VDS_INLINE void rotate_back(Arr &A) {
+  if constexpr (ROT)
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q)
+      if (q & 7) A[q] = rotl32(A[q], 32 - (q & 7));
 }
 
 // 32x32 bit transpose in place: afterwards A[p] bit i == before A[i] bit p.
+template <bool ROT = true>
 VDS_INLINE void transpose32(uint32_t (&A)[32], const BitMasks &bm = bit_masks()) {
   // j = 16: swap (row k, bits 16..31) <-> (row k+16, bits 0..15)
 #pragma unroll
@@ -322,13 +358,15 @@ VDS_INLINE void transpose32(uint32_t (&A)[32], const BitMasks &bm = bit_masks())
 #endif
     }
   // j = 4, 2, 1 : bitfield inserts
-  transpose_round<4, 32>(A, bm);
-  transpose_round<2, 32>(A, bm);
-  transpose_round<1, 32>(A, bm);
+  transpose_round<4, 32, ROT>(A, bm);
+  transpose_round<2, 32, ROT>(A, bm);
+  transpose_round<1, 32, ROT>(A, bm);
+  rotate_back<32, ROT>(A);
 }
 
 // Two independent 16x16 bit transposes held in the low / high halves of 16
 // words: afterwards A[q] bit (16h + j) == before A[j] bit (16h + q).
+template <bool ROT = true>
 VDS_INLINE void transpose16x2(uint32_t (&A)[16], const BitMasks &bm = bit_masks()) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -341,9 +379,10 @@ VDS_INLINE void transpose16x2(uint32_t (&A)[16], const BitMasks &bm = bit_masks(
     A[k + 8] = ((a >> 8) & 0x00FF00FFu) | (b & 0xFF00FF00u);
 #endif
   }
-  transpose_round<4, 16>(A, bm);
-  transpose_round<2, 16>(A, bm);
-  transpose_round<1, 16>(A, bm);
+  transpose_round<4, 16, ROT>(A, bm);
+  transpose_round<2, 16, ROT>(A, bm);
+  transpose_round<1, 16, ROT>(A, bm);
+  rotate_back<16, ROT>(A);
 }
 
 }  // namespace vds_ec

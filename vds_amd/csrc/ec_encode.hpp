@@ -22,6 +22,11 @@ namespace vds_ec {
 #define VDS_ENC_PLAN_LS 1  // local search after the LPT pair plan (plan_pairs)
 #endif
 
+// Transposes on rotated words (bitslice.hpp transpose_round) except at k =
+// 32, whose encode measured 2.8% slower with them (9.45-9.51 -> 9.72-9.78
+// ms at 256 x 64 MiB; k = 16 unchanged, profiles/round5/ab_transpose.log).
+constexpr bool enc_rot(int K) { return K != 32; }
+
 // VALU cost of one row-form Horner step for replica r (bitslice.hpp): used
 // to balance replicas across waves.
 constexpr int horner_cost(int r) { return r == 0 ? 1 : row_horner_cost((uint32_t)r); }
@@ -262,11 +267,12 @@ __device__ __forceinline__ uint8_t *rep_ptr(const FastEncodeArgs &, int r) {
 // (low half) and l + 1024 + 64 q (high half); each half goes out as a 2-byte
 // store (global_store_short / _d16_hi), so one wave-instruction writes 128
 // contiguous bytes and no cross-lane shuffle is needed.
+template <bool ROT>
 __device__ __forceinline__ void store_replica(const Plane16 &acc, uint8_t *base, const BitMasks &bm) {
   uint32_t rows[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) rows[j] = acc.p[j ^ 8];  // word bit j <-> cell bit j^8 (BE)
-  transpose16x2(rows, bm);
+  transpose16x2<ROT>(rows, bm);
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     *reinterpret_cast<uint16_t *>(base + 128 * q) = (uint16_t)rows[q];
@@ -304,13 +310,13 @@ __device__ __forceinline__ TilePos tile_pos(const FastEncodeArgs &a, uint32_t ti
 // 2s + 128j + 1, so output word j (low half = slot j, high half = slot 16 + j,
 // transpose16x2) is the 4 bytes of stripes 2s, 2s+1 of group j: one dword
 // store per word, 256 contiguous bytes per wave-instruction.
-template <bool STREAM>
+template <bool STREAM, bool ROT>
 __device__ __forceinline__ void store_replica_groups(const Plane16 &acc, uint8_t *rep, const FastEncodeArgs &a,
                                                      TilePos tp, int lane, const BitMasks &bm) {
   uint32_t rows[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) rows[j] = acc.p[j ^ 8];  // word bit j <-> cell bit j^8 (BE)
-  transpose16x2(rows, bm);
+  transpose16x2<ROT>(rows, bm);
   // (replica strides L = 2T + 2 leave odd objects 2-byte aligned: gfx950
   // global stores need no natural alignment, tested by the strided batches)
   // The trailer (trailer0): when group j is its object's last, lane 0 also
@@ -337,13 +343,13 @@ __device__ __forceinline__ void store_replica_groups(const Plane16 &acc, uint8_t
   }
 }
 
-template <int MAP, bool STREAM>
+template <int MAP, bool STREAM, bool ROT>
 __device__ __forceinline__ void store_rep(const Plane16 &acc, uint8_t *rep, const FastEncodeArgs &a, TilePos tp,
                                           int lane, const BitMasks &bm) {
   if constexpr (MAP == 0)  // k = 4: whole tiles of one object
-    store_replica(acc, rep + (uint64_t)tp.o * a.out_stride + 256u * tp.q + 2 * lane, bm);
+    store_replica<ROT>(acc, rep + (uint64_t)tp.o * a.out_stride + 256u * tp.q + 2 * lane, bm);
   else
-    store_replica_groups<STREAM>(acc, rep, a, tp, lane, bm);
+    store_replica_groups<STREAM, ROT>(acc, rep, a, tp, lane, bm);
 }
 
 // Wave priority while a pass issues its stores (same-box A/B, 512 objects:
@@ -383,7 +389,7 @@ __device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const Fa
 #pragma unroll
     for (int s = S0; s < S0 + PR && s < RPW; ++s)
       if (S::kPlan.rep[W][s] == 0)
-        store_rep<S::kMap, ST>(lds_planes(set_planes + S::cell_off(0)), rep_ptr(a, 0), a, tp, lane, bm);
+        store_rep<S::kMap, ST, enc_rot(K)>(lds_planes(set_planes + S::cell_off(0)), rep_ptr(a, 0), a, tp, lane, bm);
     return;
   }
   Plane16 A[PR], B[PR];
@@ -405,8 +411,8 @@ __device__ __forceinline__ void encode_pass(const uint32_t *set_planes, const Fa
 #pragma unroll
   for (int s = 0; s < PR; ++s) {
     const int r = S0 + s < RPW ? S::kPlan.rep[W][S0 + s] : -1;
-    if (r == 0) store_rep<S::kMap, ST>(xa, rep_ptr(a, 0), a, tp, lane, bm);
-    if (r > 0) store_rep<S::kMap, ST>(A[s], rep_ptr(a, r), a, tp, lane, bm);
+    if (r == 0) store_rep<S::kMap, ST, enc_rot(K)>(xa, rep_ptr(a, 0), a, tp, lane, bm);
+    if (r > 0) store_rep<S::kMap, ST, enc_rot(K)>(A[s], rep_ptr(a, r), a, tp, lane, bm);
   }
   __builtin_amdgcn_s_setprio(0);
 }
@@ -450,7 +456,7 @@ __device__ __forceinline__ void encode_zero_dispatch(int wave, const FastEncodeA
 #pragma unroll
       for (int s = 0; s < RPW; ++s)
         if (S::kPlan.rep[W][s] >= 0)
-          store_rep<S::kMap, ST>(plane_zero(), rep_ptr(a, S::kPlan.rep[W][s]), a, tp, lane, bm);
+          store_rep<S::kMap, ST, enc_rot(K)>(plane_zero(), rep_ptr(a, S::kPlan.rep[W][s]), a, tp, lane, bm);
     } else {
       encode_zero_dispatch<K, N, RPW, WV, ST, W + 1>(wave, a, tp, lane, bm);
     }
@@ -557,8 +563,8 @@ __device__ __forceinline__ void encode_pair_group(const uint32_t *set_planes, co
           // (round 4, tools/runs/gpu_ab_trailer.sh): k = 16 encode 13.47 -> 13.31
           // ms (512 x 64 MiB), k = 32 / n = 40 9.50-9.53 ms either way.
           const Plane16 o0 = plane_horner_enc<(uint32_t)(r(i) >= 0 ? r(i) : 0)>(R1[i], R0[i]);  // R1 r + R0
-          store_rep<S::kMap, ST>(o0, rep_ptr(a, r(i)), a, tp, lane, bm);
-          store_rep<S::kMap, ST>(plane_xor(o0, R1[i]), rep_ptr(a, r(i) + 1), a, tp, lane, bm);
+          store_rep<S::kMap, ST, enc_rot(K)>(o0, rep_ptr(a, r(i)), a, tp, lane, bm);
+          store_rep<S::kMap, ST, enc_rot(K)>(plane_xor(o0, R1[i]), rep_ptr(a, r(i) + 1), a, tp, lane, bm);
         }
       };
       (one(std::integral_constant<int, (int)I>{}), ...);
@@ -590,8 +596,8 @@ __device__ __forceinline__ void pair_zero_dispatch(int wave, const FastEncodeArg
 #pragma unroll
       for (int s = 0; s < S::kPPW; ++s)
         if (S::kPairs.r[W][s] >= 0) {
-          store_rep<S::kMap, ST>(plane_zero(), rep_ptr(a, S::kPairs.r[W][s]), a, tp, lane, bm);
-          store_rep<S::kMap, ST>(plane_zero(), rep_ptr(a, S::kPairs.r[W][s] + 1), a, tp, lane, bm);
+          store_rep<S::kMap, ST, enc_rot(K)>(plane_zero(), rep_ptr(a, S::kPairs.r[W][s]), a, tp, lane, bm);
+          store_rep<S::kMap, ST, enc_rot(K)>(plane_zero(), rep_ptr(a, S::kPairs.r[W][s] + 1), a, tp, lane, bm);
         }
     } else {
       pair_zero_dispatch<K, N, RPW, WV, ST, W + 1>(wave, a, tp, lane, bm);
@@ -682,11 +688,11 @@ __device__ __forceinline__ void encode_quad_group(const uint32_t *set_planes, co
       const Plane16 p0y1 = plane_xor(p0y0, B0);
       __builtin_amdgcn_s_setprio(kEncStorePrio);
       const Plane16 r0 = plane_horner_enc<(uint32_t)(4 * j)>(p1y0, p0y0);
-      store_rep<S::kMap, ST>(r0, rep_ptr(a, 4 * j), a, tp, lane, bm);
-      store_rep<S::kMap, ST>(plane_xor(r0, p1y0), rep_ptr(a, 4 * j + 1), a, tp, lane, bm);
+      store_rep<S::kMap, ST, enc_rot(K)>(r0, rep_ptr(a, 4 * j), a, tp, lane, bm);
+      store_rep<S::kMap, ST, enc_rot(K)>(plane_xor(r0, p1y0), rep_ptr(a, 4 * j + 1), a, tp, lane, bm);
       const Plane16 r2 = plane_horner_enc<(uint32_t)(4 * j + 2)>(p1y1, p0y1);
-      store_rep<S::kMap, ST>(r2, rep_ptr(a, 4 * j + 2), a, tp, lane, bm);
-      store_rep<S::kMap, ST>(plane_xor(r2, p1y1), rep_ptr(a, 4 * j + 3), a, tp, lane, bm);
+      store_rep<S::kMap, ST, enc_rot(K)>(r2, rep_ptr(a, 4 * j + 2), a, tp, lane, bm);
+      store_rep<S::kMap, ST, enc_rot(K)>(plane_xor(r2, p1y1), rep_ptr(a, 4 * j + 3), a, tp, lane, bm);
       __builtin_amdgcn_s_setprio(0);
     }
     encode_quad_group<K, N, RPW, WV, W, ST, S0 + 1>(set_planes, a, tp, lane, bm);
@@ -717,7 +723,7 @@ __device__ __forceinline__ void quad_zero_dispatch(int wave, const FastEncodeArg
         if (S::kQuads.j[W][s] >= 0)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            store_rep<S::kMap, ST>(plane_zero(), rep_ptr(a, 4 * S::kQuads.j[W][s] + r), a, tp, lane, bm);
+            store_rep<S::kMap, ST, enc_rot(K)>(plane_zero(), rep_ptr(a, 4 * S::kQuads.j[W][s] + r), a, tp, lane, bm);
     } else {
       quad_zero_dispatch<K, N, RPW, WV, ST, W + 1>(wave, a, tp, lane, bm);
     }
@@ -852,7 +858,7 @@ void k_encode_bs(FastEncodeArgs a) {
     }
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      transpose32(R[g], bm);
+      transpose32<enc_rot(K)>(R[g], bm);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll

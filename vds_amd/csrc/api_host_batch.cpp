@@ -34,15 +34,6 @@ uint8_t *pinned_device_ptr(const void *p, uint64_t len) {
   return d + (a - it->first);
 }
 
-// The D2H of a pinned slab by the push kernel (default) or by the copy
-// engine (VDS_EC_PIN_D2H=dma, A/B).
-bool pinned_d2h_dma() {
-  static const bool dma = [] {
-    const char *v = std::getenv("VDS_EC_PIN_D2H");
-    return v && std::strcmp(v, "dma") == 0;
-  }();
-  return dma;
-}
 
 // ------------------------------------------------- multi-GPU host batch
 // Host-resident objects, many per launch: runs of consecutive objects of one
@@ -335,7 +326,7 @@ int encode_host_batch(uint32_t k, const uint16_t *replicas, uint32_t n, const ui
     if (rc) return rc;
     if (out_dev) {  // straight into the caller's pinned slab
       s.out_parts.clear();
-      return hip_status(((reinterpret_cast<uintptr_t>(out_dev) & 15u) == 0 && !pinned_d2h_dma())
+      return hip_status(((reinterpret_cast<uintptr_t>(out_dev) & 15u) == 0)
                             ? launch_push(out_dev, s.d_out, m * n * L, s.stream)
                             : hipMemcpyAsync(out0, s.d_out, m * n * L, hipMemcpyDeviceToHost, s.stream));
     }
@@ -414,7 +405,7 @@ int restore_host_batch(uint32_t k, const uint16_t *nodes, const uint8_t *const *
     if (rc) return rc;
     s.out_parts.clear();
     if (out_dev)  // straight into the caller's pinned slab
-      return hip_status(((reinterpret_cast<uintptr_t>(out_dev) & 15u) == 0 && !pinned_d2h_dma())
+      return hip_status(((reinterpret_cast<uintptr_t>(out_dev) & 15u) == 0)
                             ? launch_push(out_dev, s.d_out, m * cap, s.stream)
                             : hipMemcpyAsync(outs[g.o0], s.d_out, m * cap, hipMemcpyDeviceToHost, s.stream));
     if ((rc = s.push_out(m * cap))) return rc;

@@ -158,14 +158,7 @@ bool plan_restore_syn(uint32_t k, const uint16_t *nodes, SynRestoreArgs &sa, uin
 
 // ---------------------------------------------------------- encode core
 // The zero trailers of a launch that covers every stripe are written by the
-// bit-sliced kernel's stores (VDS_EC_ENC_TRAILER=0: by a generic launch, A/B).
-bool fold_trailers() {
-  static const bool on = [] {
-    const char *v = std::getenv("VDS_EC_ENC_TRAILER");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+// bit-sliced kernel's stores (fa.trailer0); other launches get a generic one.
 
 int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n, const uint8_t *in,
                   uint64_t size, uint64_t in_stride, uint32_t count, uint8_t *const *outs,
@@ -205,7 +198,7 @@ int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n,
       fa.total_tiles = (uint32_t)total;
       // every stripe of every object in the launch, size a multiple of 2k:
       // the zero trailers ride the bit-sliced stores (k >= 8, map 3)
-      fa.trailer0 = (fold_trailers() && trailer && k >= 8 && 128 * gpo == T && size % stripe_bytes == 0 &&
+      fa.trailer0 = (trailer && k >= 8 && 128 * gpo == T && size % stripe_bytes == 0 &&
                      total * 16 == gpo * count)
                         ? 1u
                         : 0u;
@@ -222,7 +215,7 @@ int encode_device(unsigned cb, uint32_t k, const uint16_t *replicas, uint32_t n,
   struct Part {
     uint64_t o0, cnt, t_begin;
   };
-  const bool trailers_done = fold_trailers() && fast_groups && trailer && k >= 8 && 128 * gpo == T &&
+  const bool trailers_done = fast_groups && trailer && k >= 8 && 128 * gpo == T &&
                              size % stripe_bytes == 0 && fast_groups == gpo * count;  // (fa.trailer0 above)
   Part parts[3] = {{0, trailers_done ? 0 : o_full, 128 * gpo},
                    {o_full, o_full < count ? 1u : 0u, fast_groups ? 128 * (fast_groups - o_full * gpo) : 0},

@@ -246,9 +246,10 @@ def save_temp_leg(torch, chunk, dev, stream, inp, objects, size, k, n, L, Ls, ti
         "save_temp sha"
     del rep, dig
     pip, ser = gib(objects * size, pip_gpu), gib(objects * size, ser_gpu)
-    # headline: the faster schedule, named (both kernels are VALU-heavy, so
-    # the two-stream pipeline has measured slower than serial: DESIGN.md 9.3)
-    return {"save_temp_GiBps": max(pip, ser), "save_temp_schedule": "pipelined" if pip >= ser else "serial",
+    # headline: the schedule the library's own save_temp16_host uses (serial,
+    # one stream), not the better of two per run; the two-stream pipeline is
+    # reported beside it (it has measured slower: both kernels are VALU-heavy)
+    return {"save_temp_GiBps": ser, "save_temp_schedule": "serial",
             "pipelined_GiBps": pip, "serial_GiBps": ser,
             "batches": batches, "layout": "replicas object-major [objects][n][Ls]",
             "what": "encode of replicas 0..n-1 + SHA-256 of each; pipelined: batch b's hashes on a second stream "
@@ -287,18 +288,63 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02
     sp = stream.cuda_stream
     reps_timed = max(steps, 10)  # (beside the metric: enough calls for a stable rate)
 
-    def timed(fn):
+    spreads = {}
+
+    def timed(fn, name=None):
+        """Back-to-back calls (the rate: what a caller looping on the call
+        sees) with an event before every call, so each call's stream span is
+        a sample; and, with `name`, the same call alone behind a spin kernel
+        long enough to cover its host planning, so its span is device time
+        only.  A leg whose stream span exceeds its device time is host-bound:
+        its rate then follows the host CPU, not the kernels."""
         for _ in range(max(5, warmup)):  # steady state: staging slots allocated, erased-set plans solved
             fn()
         torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps_timed + 1)]
+        host = []
         t0 = time.perf_counter()
-        e0.record(stream)
-        for _ in range(reps_timed):
+        ev[0].record(stream)
+        for i in range(reps_timed):
+            h0 = time.perf_counter()
             fn()
-        e1.record(stream)
+            host.append(time.perf_counter() - h0)
+            ev[i + 1].record(stream)
         torch.cuda.synchronize(dev)
-        return (time.perf_counter() - t0) / reps_timed, e0.elapsed_time(e1) / reps_timed * 1e-3
+        wall = (time.perf_counter() - t0) / reps_timed
+        gpu = ev[0].elapsed_time(ev[-1]) / reps_timed * 1e-3
+        if name:
+            spans = [ev[i].elapsed_time(ev[i + 1]) for i in range(reps_timed)]
+            dev_ms = []
+            for _ in range(reps_timed):  # the device alone: the call is enqueued while the stream spins
+                torch.cuda._sleep(spin_cycles(2 * max(host) * 1e3 + 2.0))
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                fn()
+                b.record(stream)
+                torch.cuda.synchronize(dev)
+                dev_ms.append(a.elapsed_time(b))
+
+            def mm(x):
+                return {"median": round(float(np.median(x)), 4), "min": round(float(min(x)), 4),
+                        "max": round(float(max(x)), 4)}
+            spreads[name] = {"stream_ms_per_call": mm(spans), "device_ms_per_call": mm(dev_ms),
+                             "host_enqueue_ms_per_call": mm([h * 1e3 for h in host]), "calls": reps_timed,
+                             "bound": "host" if np.median(spans) > 1.1 * np.median(dev_ms) else "device"}
+        return wall, gpu
+
+    spin = {}
+
+    def spin_cycles(ms):
+        """torch.cuda._sleep cycles for about `ms` milliseconds (calibrated once)."""
+        if "per_ms" not in spin:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(stream):
+                a.record(stream)
+                torch.cuda._sleep(10 ** 7)
+                b.record(stream)
+            torch.cuda.synchronize(dev)
+            spin["per_ms"] = 10 ** 7 / max(a.elapsed_time(b), 1e-3)
+        return int(spin["per_ms"] * ms)
 
     def enc():
         chunk.encode_device(k, list(range(n)), inp, size, size, objects, rep_ptrs, Ls)
@@ -324,8 +370,8 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02
                 "frac": round(nbytes / t / 1e9 / HBM_PEAK_GBPS, 4), "bytes": what}
 
     with torch.cuda.stream(stream):
-        enc_wall, enc_gpu = timed(enc)
-        sha_wall, sha_gpu = timed(sha)
+        enc_wall, enc_gpu = timed(enc, "encode")
+        sha_wall, sha_gpu = timed(sha, "sha256")
     torch.cuda.synchronize(dev)
     enc_bytes, sha_bytes = objects * (size + n * L), n * objects * (L + 32)
     res = {"shape": f"k={k}, n={n}, {objects} x 64 KiB objects, replica stride {Ls} B",
@@ -377,8 +423,8 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02
         out.zero_()
         rg_out.zero_()
         with torch.cuda.stream(stream):
-            rest_wall, rest_gpu = timed(restore)
-            regen_wall, regen_gpu = timed(regen) if len(rg) else (None, None)
+            rest_wall, rest_gpu = timed(restore, f"repair_{loss}")
+            regen_wall, regen_gpu = timed(regen, f"regenerate_{loss}") if len(rg) else (None, None)
         torch.cuda.synchronize(dev)
         idx = torch.from_numpy(objs).to(dev)
         assert torch.equal(out.view(objects, size)[idx], inp.view(objects, size)[idx]), f"live restore differs (p={loss})"
@@ -394,13 +440,15 @@ def live_shape(torch, chunk, dev, stream, objects, steps, warmup=3, losses=(0.02
                "regenerate_GiBps": gib(len(rg) * size, regen_gpu),
                "regenerate_host_GiBps": gib(len(rg) * size, regen_wall),
                "distinct_survivor_sets": int(len({tuple(r) for r in nodes.tolist()})),
-               "survivors_within_0_39": syn_pts}
+               "survivors_within_0_39": syn_pts,
+               "spread": {"repair": spreads.get(f"repair_{loss}"), "regenerate": spreads.get(f"regenerate_{loss}")}}
         if loss == losses[0]:  # (the round-2 keys: the first loss rate)
-            res.update({kk: v for kk, v in leg.items() if kk not in ("loss", "roofline")})
+            res.update({kk: v for kk, v in leg.items() if kk not in ("loss", "roofline", "spread")})
             res["roofline"].update(leg["roofline"])
             res["shape"] += f"; replica loss p={loss}; {len(objs)} restorable, {len(rg)} regenerated"
         res[f"loss_{loss}"] = leg
         del rg_out
+    res["spread"] = {"encode": spreads.get("encode"), "sha256": spreads.get("sha256")}
     del inp, reps, out
     return res
 

@@ -251,7 +251,7 @@ int vds_ec_sha256_device(const uint8_t *base, uint64_t len, uint64_t stride, uin
  * body hash (server_api.cpp:16) is a single chain of dependent compressions,
  * ~3 us a block in one GPU lane, so vds_ec_save_temp16_host computes it here
  * while the device encodes and names the replicas.  x86 SHA extensions when
- * the CPU has them (VDS_EC_HOST_SHA=portable forces the portable code).     */
+ * the CPU has them, else portable code (FIPS 180-4 6.2).                     */
 int vds_ec_sha256_host(const uint8_t *data, uint64_t len, uint8_t *digest);
 /* vds_ec_encode16_host plus the SHA-256 of every replica, computed on the
  * device before the copy-back: digests receives n*32 bytes (host).          */
@@ -312,7 +312,7 @@ int vds_ec_fill_splitmix_device(uint8_t *dst, uint64_t size, uint64_t seed, void
  * groups ride it in batches), 1 = generic path only.  The restore query takes
  * the trailer's padding and the batch's object count, as
  * vds_ec_restore16_device does (restore planning is shared with it).
- * VDS_EC_RESTORE_PATH=bs in the environment disables path 3 (A/B).          */
+ * (A -DVDS_RESTORE_PATH_BS=1 build of the library disables path 3: A/B.)  */
 int vds_ec_encode16_path(uint16_t k, const uint16_t *replicas, uint32_t n, uint64_t size);
 int vds_ec_restore16_path(uint16_t k, const uint16_t *nodes, uint64_t chunk_size, uint16_t padding, uint32_t count);
 /* 4 = the regenerate runs the survivor set's run-time compiled kernel
@@ -339,11 +339,16 @@ int vds_ec_regenerate16_path(uint16_t k, const uint16_t *nodes, const uint16_t *
  * vds_ec_jit_build16: compile the kernel of survivor set `nodes` and return
  *                     its code object size (no device needed; EINVAL for a set
  *                     the syndrome kernel does not serve, EHIP if hiprtc fails).
- * vds_ec_jit_ready16: 1 when that set's kernel is compiled, else 0.          */
+ * vds_ec_jit_ready16: 1 when that set's kernel is compiled, else 0.
+ * vds_ec_jit_dump16:  compile the kernel of survivor set `nodes` (regen != 0:
+ *                     its fused-regenerate kernel) and write its source and
+ *                     code object as dir/jit_<k>_<n>_<mask>[_regen].{hip,co}
+ *                     (inspection: register use, spills; no device needed).  */
 int vds_ec_jit_set_mode(int mode);
 int vds_ec_jit_wait(void);
 int vds_ec_jit_build16(uint16_t k, const uint16_t *nodes, uint64_t *code_bytes);
 int vds_ec_jit_ready16(uint16_t k, const uint16_t *nodes);
+int vds_ec_jit_dump16(uint16_t k, const uint16_t *nodes, int regen, const char *dir);
 
 #ifdef __cplusplus
 }

@@ -42,10 +42,11 @@ def test_jit_kernel_symbol_names_its_set(tmp_path):
     """The run-time kernels are named by kind, (k, n) and survivor mask
     (vds_ec_jit.cpp kernel_name), so rocprofv3 summaries separate the
     headline set's kernel from every other instantiation."""
-    code = ("from vds_amd import chunk\n"
-            "print(chunk.jit_build(16, [r for r in range(20) if r not in (0, 5, 10, 15)]))\n")
-    env = dict(os.environ, VDS_EC_JIT_DUMP=str(tmp_path), VDS_EC_JIT_CACHE="0")
-    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    code = ("import sys\nfrom vds_amd import chunk\n"
+            "chunk.jit_dump(16, [r for r in range(20) if r not in (0, 5, 10, 15)], sys.argv[1])\n")
+    env = dict(os.environ, VDS_EC_JIT_CACHE="0")
+    r = subprocess.run([sys.executable, "-c", code, str(tmp_path)], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     cos = list(tmp_path.glob("*.co"))
     assert len(cos) == 1

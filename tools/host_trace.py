@@ -1,6 +1,7 @@
 """Host planning cost of the live shape's batched restore / regenerate
-(VDS_EC_HOST_TRACE=1 prints each call's phases to stderr).
-  VDS_EC_HOST_TRACE=1 python tools/host_trace.py [--loss 0.02] [--objects 16384]"""
+(a library built with -DVDS_HOST_TRACE=1 prints each call's phases to stderr).
+  python -c "from vds_amd import build as b; b.build(out='ab/trace/libvds_ec.so', defines=('-DVDS_HOST_TRACE=1',))"
+  VDS_EC_LIB=ab/trace/libvds_ec.so python tools/host_trace.py [--loss 0.02] [--objects 16384]"""
 import argparse
 import os
 import sys

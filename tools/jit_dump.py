@@ -54,17 +54,15 @@ def main() -> int:
         nodes = [r for r in range(n) if r % step][:k]
     d = a.keep or tempfile.mkdtemp(prefix="jit_dump_")
     os.makedirs(d, exist_ok=True)
-    os.environ["VDS_EC_JIT_DUMP"] = d
     os.environ["VDS_EC_JIT_CACHE"] = "0"
     lib = C.CDLL(a.lib)
     arr = (C.c_uint16 * k)(*nodes)
-    nb = C.c_uint64(0)
-    rc = lib.vds_ec_jit_build16(C.c_uint16(k), arr, C.byref(nb))
+    rc = lib.vds_ec_jit_dump16(C.c_uint16(k), arr, C.c_int(0), os.fsencode(d))
     if rc != 0:
         print("build failed", rc, file=sys.stderr)
         return 1
     for co in sorted(glob.glob(os.path.join(d, "*.co"))):
-        print(os.path.basename(co), nb.value, "bytes", resources(co))
+        print(os.path.basename(co), os.path.getsize(co), "bytes", resources(co))
     return 0
 
 

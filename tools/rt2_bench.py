@@ -1,7 +1,8 @@
 """RT batch restore at the live shape with a fixed number of erased points
 below k per object (every object on the RT route): GPU time per call and a
-check of every restored object against the encoded input.  Run twice, with
-VDS_EC_RT2=1 (default) and VDS_EC_RT2=0, for the RT2 rows A/B.
+check of every restored object against the encoded input.  Run with the
+default library and with a -DVDS_BATCH_RT2=0 build (VDS_EC_LIB=...) for the
+RT2 rows A/B.
   python tools/rt2_bench.py [--objects 16384] [--rows 8] [--steps 10]"""
 import argparse
 import json
@@ -64,14 +65,14 @@ for _ in range(a.steps):
 e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / a.steps
-print(json.dumps({"rt2": os.environ.get("VDS_EC_RT2", "1"), "rows": a.rows, "objects": objects, "ms_per_call": round(ms, 4),
+print(json.dumps({"lib": os.environ.get("VDS_EC_LIB", "default"), "rows": a.rows, "objects": objects, "ms_per_call": round(ms, 4),
                   "GiBps": round(objects * size / (ms * 1e-3) / 2**30, 2)}))
 
 # VDS_EC_LIB = a -DVDS_DIAG_STAMPS=1 build: the per-phase ticks of the last call
 if hasattr(lib, "vds_ec_diag_stamps"):
     import ctypes as C
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    NPH, WV, grid = 20, 8, 256
+    NPH, WV, grid = 24, 8, 256
     buf = np.zeros(4096 * 4 * NPH, dtype=np.uint64)
     torch.cuda.synchronize()
     assert lib.vds_ec_diag_stamps(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), C.c_size_t(buf.size)) == 0

@@ -24,7 +24,7 @@ from vds_amd import _lib, chunk  # noqa: E402
 PHASES = ["stage1 transposes+puts", "B1", "syndrome+load issue", "recovery walk", "B2", "ds_xor scatter", "B3",
           "stage A", "B(stage A)", "stage B programs", "B(Q read)", "P0/P1 puts", "B(P put)", "stage C",
           "B(stage C read)", "staging transposes+writes", "B(staging)", "copy-out stores", "B(tile end)", "-"]
-NPH = 20
+NPH = 24
 
 p = argparse.ArgumentParser()
 p.add_argument("--objects", type=int, default=128)
@@ -69,3 +69,24 @@ print(f"{'phase':28s} " + " ".join(f"{'w%d' % w:>8s}" for w in range(WV)) + f" {
 for ph in range(19):
     col = st[:, :, ph].mean(axis=0)
     print(f"{PHASES[ph]:28s} " + " ".join(f"{c:8.0f}" for c in col) + f" {col.mean():8.0f} {100 * col.mean() / tot:6.1f}")
+
+# Phase coherence across CUs (slots 20..23: s_memrealtime, the chip-global
+# 100 MHz clock, at wave 0's survivor-load issue of its tiles 4, 64, 160, 240).
+# Each workgroup's phase is its issue time modulo the median tile period; R is
+# the length of the mean phase vector (1: every CU issues its loads in the
+# same instant of the period, ~0: spread evenly over the period).
+ITERS = [4, 64, 160, 240]
+rt = buf[: grid * WV * NPH].reshape(grid, WV, NPH)[:, 0, 20:24].astype(np.int64)
+ok = [j for j in range(4) if ITERS[j] < per_block and (rt[:, j] > 0).all()]
+if len(ok) >= 2:
+    j0, j1 = ok[0], ok[-1]
+    period = np.median((rt[:, j1] - rt[:, j0]) / (ITERS[j1] - ITERS[j0]))
+    print(f"\nload-issue phase across {grid} workgroups (tile period {period * 10:.0f} ns, median):")
+    odd = ((np.arange(grid) >> 3) & 1).astype(bool)
+    for j in ok:
+        ph = ((rt[:, j] - np.median(rt[:, j])) / period) % 1.0
+        vec = np.exp(2j * np.pi * ph)
+        hist = np.histogram(ph, bins=8, range=(0, 1))[0]
+        print(f"  tile {ITERS[j]:4d}: R = {abs(vec.mean()):.3f}  (even half {abs(vec[~odd].mean()):.3f}, odd half "
+              f"{abs(vec[odd].mean()):.3f}, odd-even offset {np.angle(vec[odd].mean() / vec[~odd].mean()) / (2 * np.pi):+.2f}"
+              f" period)  phase histogram (8 bins) {hist.tolist()}")

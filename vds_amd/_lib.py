@@ -79,6 +79,7 @@ SIGNATURES = {
     "vds_ec_jit_wait": (C.c_int, []),
     "vds_ec_jit_build16": (C.c_int, [C.c_uint16, u16p, u64p]),
     "vds_ec_jit_ready16": (C.c_int, [C.c_uint16, u16p]),
+    "vds_ec_jit_dump16": (C.c_int, [C.c_uint16, u16p, C.c_int, C.c_char_p]),
     "vds_ec_restore16_batch_device": (C.c_int, [C.c_uint16, C.c_uint32, u16p, vpp, u64p, u16p, vpp, C.c_uint,
                                                 C.c_void_p]),
     "vds_ec_regenerate16_batch_device": (C.c_int, [C.c_uint16, C.c_uint32, u16p, vpp, u64p, C.c_uint32, u16p, vpp,

@@ -117,11 +117,34 @@ def _local_includes(path: str, seen: set[str]) -> None:
                 break
 
 
+_TOOLCHAIN: str | None = None
+
+
+def _toolchain_id() -> str:
+    """Identity of the compiler (hipcc --version and the clang binary's path,
+    size and mtime), computed once per process: an in-place ROCm upgrade
+    behind the same hipcc path must not reuse objects built by the old one."""
+    global _TOOLCHAIN
+    if _TOOLCHAIN is None:
+        hipcc = _hipcc()
+        try:
+            ver = subprocess.run([hipcc, "--version"], capture_output=True, text=True, timeout=60).stdout
+        except (OSError, subprocess.SubprocessError):
+            ver = "?"
+        rocm = os.path.dirname(os.path.dirname(os.path.realpath(hipcc)))
+        clang = os.path.realpath(os.path.join(rocm, "lib", "llvm", "bin", "clang"))
+        st = os.stat(clang) if os.path.exists(clang) else None
+        _TOOLCHAIN = f"{ver}|{clang}|{st.st_size if st else 0}|{st.st_mtime_ns if st else 0}"
+    return _TOOLCHAIN
+
+
 def _obj_key(cmd: list[str], src: str) -> str:
-    """Hash of the compile command (minus the output path) and of the bytes of
-    the source and every local header it includes.  A -D define whose macro
-    the unit never names cannot change its object and is left out, so a
-    variant build recompiles only the units its switches reach."""
+    """Hash of the toolchain identity, the compile command (minus the output
+    path) and the bytes of the source and every local header it includes.  A
+    project switch (-DVDS_...) that the unit never names cannot change its
+    object and is left out, so a variant build recompiles only the units its
+    switches reach; every other -D is kept (it may act through a system
+    header, e.g. NDEBUG)."""
     files: set[str] = set()
     _local_includes(os.path.join(CSRC, src), files)
     texts = []
@@ -129,8 +152,14 @@ def _obj_key(cmd: list[str], src: str) -> str:
         with open(f, "rb") as fh:
             texts.append((f, fh.read()))
     blob = b"".join(t for _, t in texts)
-    args = [a for a in cmd[:-2] if not (a.startswith("-D") and a[2:].split("=")[0].encode() not in blob)]
+
+    def unused_switch(a: str) -> bool:
+        name = a[2:].split("=")[0]
+        return a.startswith("-DVDS_") and name.encode() not in blob
+
+    args = [a for a in cmd[:-2] if not unused_switch(a)]
     h = hashlib.sha256()
+    h.update(_toolchain_id().encode())
     h.update("\0".join(args).encode())
     for f, t in texts:
         h.update(f.encode())
@@ -138,8 +167,12 @@ def _obj_key(cmd: list[str], src: str) -> str:
     return h.hexdigest()[:32]
 
 
-def _cached_compile(cmd: list[str], obj: str, key: str) -> None:
-    """Compile unless an object with the same key is cached; keep the result."""
+def _cached_compile(cmd: list[str], obj: str, key: str | None) -> None:
+    """Compile unless an object with the same key is cached; keep the result.
+    key None: compile, bypassing the cache (forced builds, VDS_EC_OBJCACHE=0)."""
+    if key is None:
+        subprocess.run(cmd, check=True)
+        return
     hit = os.path.join(OBJCACHE, key + ".o")
     if os.path.exists(hit):
         shutil.copyfile(hit, obj)
@@ -158,15 +191,16 @@ def _cached_compile(cmd: list[str], obj: str, key: str) -> None:
             pass
 
 
-def _compile_all(tmp: str, defines: tuple[str, ...], verbose: bool) -> list[str]:
+def _compile_all(tmp: str, defines: tuple[str, ...], verbose: bool, use_cache: bool = True) -> list[str]:
     jobs = []
     write_jit_embed(tmp)
+    use_cache = use_cache and os.environ.get("VDS_EC_OBJCACHE", "1") != "0"
     for src in SOURCES:
         obj = os.path.join(tmp, src.rsplit(".", 1)[0] + ".o")
         cmd = compile_cmd(src, obj, defines)
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        jobs.append((cmd, obj, _obj_key(cmd, src)))
+        jobs.append((cmd, obj, _obj_key(cmd, src) if use_cache else None))
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 1), 8))
     rocm = os.path.dirname(os.path.dirname(os.path.realpath(_hipcc())))
     jitc = [_hipcc(), "-O2", "-std=c++20", _arch_define(), "-I", tmp, os.path.join(CSRC, "vds_ec_jitc.cpp"), "-o",
@@ -185,7 +219,9 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None,
           defines: tuple[str, ...] = ()) -> str:
     """Build the library (default: in-tree libvds_ec.so, rebuilt when stale).
     `out` + `defines` build a variant (e.g. -DVDS_DIAG_STAMPS=1) for A/B
-    measurements; the variant is loaded with VDS_EC_LIB=<path>."""
+    measurements; the variant is loaded with VDS_EC_LIB=<path>.  force=True
+    recompiles every unit (the object cache is bypassed; VDS_EC_OBJCACHE=0
+    turns the cache off for any build)."""
     lib = out or LIB
     if out is None and not force and not _stale(lib):
         return LIB
@@ -196,7 +232,7 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None,
             if out is None and not force and not _stale(lib):
                 return LIB  # built by another process while this one waited
             with tempfile.TemporaryDirectory(prefix="vds_build_", dir=HERE) as tmp:
-                objs = _compile_all(tmp, defines, verbose)
+                objs = _compile_all(tmp, defines, verbose, use_cache=not force)
                 tmp_lib = os.path.join(tmp, "lib.so")
                 subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp_lib] + objs +
                                ["-lpthread", "-ldl"], check=True)

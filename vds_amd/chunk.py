@@ -18,6 +18,7 @@ uint8_t (1) instantiation.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Dict, Iterable, Mapping, Sequence
 
 import numpy as np
@@ -502,6 +503,13 @@ def jit_build(k: int, nodes: Sequence[int]) -> int:
 def jit_ready(k: int, nodes: Sequence[int]) -> bool:
     a = _ids(nodes, 2)
     return bool(_lib.lib().vds_ec_jit_ready16(k, _idp(a, 2)))
+
+
+def jit_dump(k: int, nodes: Sequence[int], directory: str, regen: bool = False) -> None:
+    """Compile (no device needed) the kernel of survivor set `nodes` and write
+    its source and code object into `directory` (vds_ec_jit_dump16)."""
+    a = _ids(nodes, 2)
+    check(_lib.lib().vds_ec_jit_dump16(k, _idp(a, 2), 1 if regen else 0, os.fsencode(directory)))
 
 
 def fill_splitmix_device(dst, size: int, seed: int, stream=None) -> None:

@@ -247,15 +247,12 @@ struct BatchObjInfo {
 // target in k..2k-1)
 constexpr uint8_t kMsPerm = 3;
 
-// The SMALL batch kernels (VDS_EC_SMALL=0 routes their objects to the
-// N = k + k/4 syndrome kernel instead: A/B).
-bool small_enabled() {
-  static const bool on = [] {
-    const char *v = std::getenv("VDS_EC_SMALL");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+// The SMALL batch kernels (a -DVDS_BATCH_SMALL=0 build routes their objects
+// to the N = k + k/4 syndrome kernel instead: A/B).
+#ifndef VDS_BATCH_SMALL
+#define VDS_BATCH_SMALL 1
+#endif
+constexpr bool small_enabled() { return VDS_BATCH_SMALL != 0; }
 // The smallest SMALL ms whose points 0..k+ms-1 hold every survivor (maxid), or 0.
 uint8_t small_ms_for(uint32_t k, uint32_t maxid) {
   if (!small_enabled()) return 0;
@@ -496,15 +493,12 @@ struct SynBatchBuild {
 // halves are paired in order of row count.  One pinned slot holds the
 // objects, the tiles and -- device side only, written by the coefficient
 // kernel -- the rows.  fill() may run on several threads for distinct i.
-// RT2 rows for the k = 32 restore's RT objects (VDS_EC_RT2=0: every RT
-// object takes the k-slot combination, A/B)
-bool rt2_enabled() {
-  static const bool on = [] {
-    const char *v = std::getenv("VDS_EC_RT2");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+// RT2 rows for the k = 32 restore's RT objects (a -DVDS_BATCH_RT2=0 build:
+// every RT object takes the k-slot combination, A/B)
+#ifndef VDS_BATCH_RT2
+#define VDS_BATCH_RT2 1
+#endif
+constexpr bool rt2_enabled() { return VDS_BATCH_RT2 != 0; }
 
 struct RtBatchBuild {
   uint32_t k, n;
@@ -671,8 +665,11 @@ struct BatchIndex {
   }
 };
 
-// VDS_EC_HOST_TRACE=1: the batched calls print their host phases (us) to
-// stderr (planning cost study).
+// A -DVDS_HOST_TRACE=1 build: the batched calls print their host phases (us)
+// to stderr (planning cost study, tools/host_trace.py).
+#ifndef VDS_HOST_TRACE
+#define VDS_HOST_TRACE 0
+#endif
 struct HostTrace {
   const char *name;
   bool on;
@@ -682,10 +679,7 @@ struct HostTrace {
   explicit HostTrace(const char *n) : name(n), on(enabled()) {
     if (on) t0 = last = std::chrono::steady_clock::now();
   }
-  static bool enabled() {
-    static const bool e = std::getenv("VDS_EC_HOST_TRACE") != nullptr;
-    return e;
-  }
+  static constexpr bool enabled() { return VDS_HOST_TRACE != 0; }
   void mark(const char *phase) {
     if (!on) return;
     const auto now = std::chrono::steady_clock::now();

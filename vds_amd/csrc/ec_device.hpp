@@ -7,7 +7,6 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
-#include <cstdlib>
 #endif
 #include <cstdint>
 
@@ -115,12 +114,19 @@ __device__ __forceinline__ TileRange tile_range(uint32_t total) {
 // ------------------------------------------------------------ host helpers
 #ifndef __HIPCC_RTC__
 
-// Study override of a fast kernel's grid (workgroups), read once per launcher:
-// VDS_EC_ENC_GRID / VDS_EC_SYN_GRID (0 or unset = the default sizing).
-inline uint32_t grid_override(const char *name) {
-  const char *v = std::getenv(name);
-  return v ? (uint32_t)std::strtoul(v, nullptr, 10) : 0u;
-}
+// Study overrides of the fast kernels' grids (workgroups), compile-time:
+// -DVDS_ENC_GRID=n / -DVDS_SYN_GRID=n (0 = the default sizing), and
+// -DVDS_ENC_LDS_EXTRA=bytes of unused LDS per encode workgroup (runs the
+// encode at fewer workgroups per CU; diagnostic).
+#ifndef VDS_ENC_GRID
+#define VDS_ENC_GRID 0
+#endif
+#ifndef VDS_SYN_GRID
+#define VDS_SYN_GRID 0
+#endif
+#ifndef VDS_ENC_LDS_EXTRA
+#define VDS_ENC_LDS_EXTRA 0
+#endif
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):
 // the attribute is per device, and the multi-GPU host batches launch from one

@@ -900,30 +900,29 @@ void k_encode_bs(FastEncodeArgs a) {
 template <int K, int N, int RPW, int WV, bool STREAM, bool SPLIT, bool QUAD>
 static hipError_t launch_encode_bs_st(const FastEncodeArgs &a, hipStream_t s) {
   using S = EncodeShape<K, N, RPW, WV>;
-  // VDS_EC_ENC_LDS_EXTRA: extra (unused) LDS bytes per workgroup, to measure
-  // the kernel at fewer workgroups per CU (diagnostic)
-  static const uint32_t extra = grid_override("VDS_EC_ENC_LDS_EXTRA");
-  const int lds = S::kLdsBytes + (int)(extra < 64 * 1024 ? extra : 0);
+  // VDS_ENC_LDS_EXTRA: extra (unused) LDS bytes per workgroup, to measure
+  // the kernel at fewer workgroups per CU (diagnostic, ec_device.hpp)
+  static_assert(VDS_ENC_LDS_EXTRA >= 0 && VDS_ENC_LDS_EXTRA < 64 * 1024, "VDS_ENC_LDS_EXTRA");
+  const int lds = S::kLdsBytes + VDS_ENC_LDS_EXTRA;
   hipError_t e = ensure_lds_attr(&k_encode_bs<K, N, RPW, WV, STREAM, SPLIT, QUAD>, lds);
   if (e != hipSuccess) return e;
   const int blocks_per_cu = (160 * 1024) / lds;
   int grid = 256 * (blocks_per_cu > 0 ? blocks_per_cu : 1);
-  static const uint32_t over = grid_override("VDS_EC_ENC_GRID");
-  if (over) grid = (int)over;
+  if (VDS_ENC_GRID > 0) grid = VDS_ENC_GRID;
   if ((uint32_t)grid > a.total_tiles) grid = (int)a.total_tiles;
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL((k_encode_bs<K, N, RPW, WV, STREAM, SPLIT, QUAD>), dim3(grid), dim3(S::kThreads), lds, s, a);
   return hipGetLastError();
 }
 
-// VDS_EC_ENCODE_PATH=horner: plain Horner where split mode is compiled;
-// =pair: the one-level split where the two-level one is the default (A/B).
-static char encode_path() {
-  static const char h = [] {
-    const char *v = std::getenv("VDS_EC_ENCODE_PATH");
-    return v ? v[0] : '\0';
-  }();
-  return h;
+// A/B builds: -DVDS_ENCODE_PATH=1 plain Horner where split mode is compiled,
+// 2 the one-level split where the two-level one is the default, 3 the
+// two-level split everywhere; 0 (default) the measured choice below.
+#ifndef VDS_ENCODE_PATH
+#define VDS_ENCODE_PATH 0
+#endif
+constexpr char encode_path() {
+  return VDS_ENCODE_PATH == 1 ? 'h' : VDS_ENCODE_PATH == 2 ? 'p' : VDS_ENCODE_PATH == 3 ? 'q' : '\0';
 }
 
 template <int K, int N, int RPW, int WV, bool SPLIT, bool QUAD>

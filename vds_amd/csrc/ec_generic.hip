@@ -380,20 +380,30 @@ static uint64_t g_tables_ready = 0;  // bit d: device d has the log / exp tables
 // Built once per device on a private stream, which this thread then waits
 // for: the caller's stream is neither synchronised nor used, so a
 // stream-ordered *_device call that gets here first still only enqueues on
-// it (and works under stream capture); every later launch on any stream sees
-// the finished tables.
+// it; every later launch on any stream sees the finished tables.
+// While a stream of the process is being captured in global mode, creating
+// and synchronising a stream are prohibited calls that would invalidate that
+// capture; this thread switches to relaxed capture mode for the build and
+// back, so the build cannot.  (Capturing the batch entry points
+// themselves in a graph is not supported: their descriptors live in pinned
+// parameter slots that later calls reuse, api_param_ring.cpp.)
 static hipError_t ensure_gf16_tables() {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> g(g_tables_mu);
   if (dev < 64 && ((g_tables_ready >> dev) & 1u)) return hipSuccess;
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  if ((e = hipThreadExchangeStreamCaptureMode(&mode)) != hipSuccess) return e;
   hipStream_t own = nullptr;
-  if ((e = hipStreamCreateWithFlags(&own, hipStreamNonBlocking)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_gf16_tables, dim3((65535 + 255) / 256), dim3(256), 0, own);
-  e = hipGetLastError();
-  if (e == hipSuccess) e = hipStreamSynchronize(own);
-  (void)hipStreamDestroy(own);
+  e = hipStreamCreateWithFlags(&own, hipStreamNonBlocking);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_gf16_tables, dim3((65535 + 255) / 256), dim3(256), 0, own);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(own);
+    (void)hipStreamDestroy(own);
+  }
+  (void)hipThreadExchangeStreamCaptureMode(&mode);  // (the caller's mode again)
   if (e != hipSuccess) return e;
   if (dev < 64) g_tables_ready |= 1ull << dev;
   return hipSuccess;

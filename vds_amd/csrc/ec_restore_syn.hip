@@ -55,8 +55,7 @@ hipError_t launch_restore_syn_jit(hipFunction_t fn, uint32_t k, uint32_t n, cons
   }
   blocks_per_cu = (160 * 1024) / lds;
   uint32_t grid = 256u * (blocks_per_cu > 0 ? blocks_per_cu : 1);
-  static const uint32_t over = grid_override("VDS_EC_SYN_GRID");
-  if (over) grid = over;
+  if (VDS_SYN_GRID > 0) grid = VDS_SYN_GRID;
   if (grid > a.total_tiles) grid = a.total_tiles;
   if (grid == 0) return hipSuccess;
   // survivors in point order: the scatter fill programs of wave w take the

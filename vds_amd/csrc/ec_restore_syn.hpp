@@ -52,8 +52,7 @@ static hipError_t launch_restore_syn_kn(const SynRestoreArgs &a, hipStream_t s) 
   if (e != hipSuccess) return e;
   const int blocks_per_cu = (160 * 1024) / S::kLdsBytes;
   uint32_t grid = 256u * (blocks_per_cu > 0 ? blocks_per_cu : 1);
-  static const uint32_t over = grid_override("VDS_EC_SYN_GRID");
-  if (over) grid = over;
+  if (VDS_SYN_GRID > 0) grid = VDS_SYN_GRID;
   if (grid > a.total_tiles) grid = a.total_tiles;
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL((k_restore_syn<K, N, WV, REGEN, BATCH, RT, FILL>), dim3(grid), dim3(S::kThreads), S::kLdsBytes, s, a);

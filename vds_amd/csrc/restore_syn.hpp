@@ -71,7 +71,11 @@ __device__ __forceinline__ void syn_prio() {
 }
 
 #if VDS_DIAG_STAMPS
-constexpr int kStampPhases = 20;
+// phases 0..19 are s_memtime sums; 20..23 hold the s_memrealtime (chip-wide
+// 100 MHz clock) at which the wave issued the survivor loads of its
+// kStampRtIter[j]-th tile, so the host can compare the CUs' phases.
+constexpr int kStampPhases = 24;
+constexpr uint32_t kStampRtIter[4] = {4, 64, 160, 240};
 constexpr int kStampSlots = 4096 * 4 * kStampPhases;
 __device__ unsigned long long g_syn_stamps[kStampSlots];
 struct Stamps {
@@ -85,6 +89,11 @@ struct Stamps {
     acc[i] += now - prev;
     prev = now;
   }
+  __device__ __forceinline__ void rt(uint32_t iter) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (iter == kStampRtIter[j]) acc[20 + j] = __builtin_amdgcn_s_memrealtime();
+  }
   __device__ __forceinline__ void flush(int slot, int lane) {
     if (lane == 0 && slot < 4096 * 4)
       for (int i = 0; i < kStampPhases; ++i) g_syn_stamps[slot * kStampPhases + i] = acc[i];
@@ -94,6 +103,7 @@ struct Stamps {
 struct Stamps {
   __device__ __forceinline__ void init() {}
   __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void rt(uint32_t) {}
   __device__ __forceinline__ void flush(int, int) {}
 };
 #endif
@@ -684,8 +694,11 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   // staying live (as loop-carried state) through the programs until the load
   // (k = 32 spilled 203 VGPRs that way: 1.6x / 1.4x the algorithmic traffic).
   const TileRange tr = tile_range(a.total_tiles);
+  Stamps st;
+  st.init();
   auto prefetch = [&](uint32_t t) {
     if (t < tr.end) {
+      st.rt((t - tr.first) / tr.step);
       load(t);
     } else {
 #pragma unroll
@@ -694,8 +707,6 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
         for (int q = 0; q < 4; ++q) Q[s][q] = u32x4{0u, 0u, 0u, 0u};
     }
   };
-  Stamps st;
-  st.init();
   // k = 32 (one 160 KiB workgroup per CU): the prefetched survivors would be
   // live across the syndrome and stage-B programs, which then spill; they are
   // issued after the interpolation instead and land under the staging and

@@ -11,14 +11,22 @@
 //
 // Two implementations, picked once: the x86 SHA extensions (sha256rnds2 /
 // sha256msg1 / sha256msg2, present on the GPU box's EPYC and on this
-// container's Xeon) and a portable one (FIPS 180-4 section 6.2);
-// VDS_EC_HOST_SHA=portable forces the latter (tests compare both with
-// hashlib).
+// container's Xeon) and a portable one (FIPS 180-4 section 6.2), the only
+// one on other hosts.  A -DVDS_HOST_SHA_PORTABLE=1 build forces the latter
+// (tests/test_sha256_host.py compiles this file both ways and compares each
+// with hashlib).
+#ifndef VDS_HOST_SHA_PORTABLE
+#define VDS_HOST_SHA_PORTABLE 0
+#endif
+#if defined(__x86_64__) || defined(__i386__)
+#define VDS_HOST_SHA_X86 1
 #include <cpuid.h>
 #include <immintrin.h>
+#else
+#define VDS_HOST_SHA_X86 0
+#endif
 
 #include <cstdint>
-#include <cstdlib>
 #include <cstring>
 
 #include "vds_ec.h"
@@ -68,6 +76,7 @@ void blocks_portable(uint32_t h[8], const uint8_t *p, size_t nblocks) {
   }
 }
 
+#if VDS_HOST_SHA_X86
 // The SHA extensions: the state lives as ABEF / CDGH in two xmm registers,
 // four rounds per pair of sha256rnds2, the schedule by sha256msg1/msg2.
 __attribute__((target("sha,sse4.1,ssse3"))) void blocks_shani(uint32_t h[8], const uint8_t *p, size_t nblocks) {
@@ -113,13 +122,15 @@ bool have_shani() {
   const bool sse41 = (c >> 19) & 1u, ssse3 = (c >> 9) & 1u;
   return sha && sse41 && ssse3;
 }
+#endif  // VDS_HOST_SHA_X86
 
 using BlocksFn = void (*)(uint32_t *, const uint8_t *, size_t);
 BlocksFn blocks_fn() {
   static const BlocksFn f = [] {
-    const char *v = std::getenv("VDS_EC_HOST_SHA");
-    if (v && !std::strcmp(v, "portable")) return (BlocksFn)blocks_portable;
-    return have_shani() ? (BlocksFn)blocks_shani : (BlocksFn)blocks_portable;
+#if VDS_HOST_SHA_X86 && !VDS_HOST_SHA_PORTABLE
+    if (have_shani()) return (BlocksFn)blocks_shani;
+#endif
+    return (BlocksFn)blocks_portable;
   }();
   return f;
 }

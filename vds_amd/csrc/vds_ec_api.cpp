@@ -87,13 +87,11 @@ int inverse8(uint32_t k, const uint8_t *nodes, uint16_t *out) {
 // values lie on exactly one polynomial of degree < K, so the recovered
 // replicas and the interpolated object equal V_S^{-1} applied to the
 // survivors (the reference's chunk.h:290-375 route) for every input.
-bool restore_path_override_bs() {
-  static const bool bs = [] {
-    const char *v = std::getenv("VDS_EC_RESTORE_PATH");
-    return v && std::strcmp(v, "bs") == 0;
-  }();
-  return bs;
-}
+// (a -DVDS_RESTORE_PATH_BS=1 build sends every restore to k_restore_bs: A/B)
+#ifndef VDS_RESTORE_PATH_BS
+#define VDS_RESTORE_PATH_BS 0
+#endif
+bool restore_path_override_bs() { return VDS_RESTORE_PATH_BS != 0; }
 
 // The syndrome kernel's point assignment for a survivor list: eligible when
 // the k ids are distinct points of 0..k+k/4-1 for a compiled (k, n); fills
@@ -1337,11 +1335,17 @@ int vds_ec_encode16_hash_host(uint16_t k, const uint16_t *replicas, uint32_t n, 
   if (rc) return rc;
   std::vector<uint8_t *> douts(n);
   for (uint32_t i = 0; i < n; ++i) douts[i] = c.d_out + (uint64_t)i * L;
+  // (an error after the first enqueue drains the stream before returning:
+  // the next call on this thread reuses c's buffers)
+  auto drained = [&](int r) {
+    (void)hipStreamSynchronize(c.stream);
+    return r;
+  };
   rc = encode_device(2, k, replicas, n, c.d_in, size, size, 1, douts.data(), 0, flags, c.stream);
-  if (rc) return rc;
+  if (rc) return drained(rc);
   // the replica hashes of save_temp / save_data (dht_network_client.cpp:79, :593), on the device
   hipError_t e = launch_sha256(c.d_out, L, L, n, c.d_out + dig, c.stream);
-  if (e != hipSuccess) return hip_status(e);
+  if (e != hipSuccess) return drained(hip_status(e));
   if ((rc = c.push_out_and_wait(dig + 32ull * n))) return rc;
   std::vector<Copy> parts(n);
   for (uint32_t i = 0; i < n; ++i) parts[i] = {outs[i], c.h_out + (uint64_t)i * L, L};
@@ -1357,39 +1361,45 @@ int vds_ec_save_temp16_host(uint16_t k, uint32_t n, const uint8_t *data, uint64_
   if (rc) return rc;
   const uint64_t L = vds_ec_replica_size(2, k, size, 0);
   if (replica_size) *replica_size = (uint32_t)L;  // save_temp: replica 0's size (dht_network_client.cpp:81-83)
+  if (n == 0) {  // only the body hash: nothing to stage or encode
+    sha256_host(data, size, data_digest);
+    return VDS_EC_OK;
+  }
   HostCtx *cp = host_ctx();
   if (!cp) return VDS_EC_ENODEV;
   HostCtx &c = *cp;
   // replicas, then n digests at a 16-byte aligned offset: one push out
   const uint64_t dig = (L * n + 15) & ~15ull;
-  rc = c.ensure(size ? size : 1, dig + 32ull * (n ? n : 1));
+  rc = c.ensure(size ? size : 1, dig + 32ull * n);
   if (!rc) rc = c.stage_in(data, size);
   if (rc) return rc;
+  // (an error after the first enqueue drains the stream before returning:
+  // the next call on this thread reuses c's buffers)
+  auto drained = [&](int r) {
+    (void)hipStreamSynchronize(c.stream);
+    return r;
+  };
   std::vector<Copy> parts;
-  if (n) {
-    std::vector<uint16_t> ids(n);
-    std::vector<uint8_t *> douts(n);
-    for (uint32_t i = 0; i < n; ++i) {
-      ids[i] = (uint16_t)i;
-      douts[i] = c.d_out + (uint64_t)i * L;
-      parts.push_back({outs[i], c.h_out + (uint64_t)i * L, L});
-    }
-    rc = encode_device(2, k, ids.data(), n, c.d_in, size, size, 1, douts.data(), 0, 0, c.stream);
-    if (rc) return rc;
-    hipError_t e = launch_sha256(c.d_out, L, L, n, c.d_out + dig, c.stream);  // save_temp's replica names (:79)
-    if (e != hipSuccess) return hip_status(e);
-    e = launch_push(c.h_out_dev, c.d_out, dig + 32ull * n, c.stream);
-    if (e != hipSuccess) return hip_status(e);
-    parts.push_back({replica_digests, c.h_out + dig, 32ull * n});
+  std::vector<uint16_t> ids(n);
+  std::vector<uint8_t *> douts(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    ids[i] = (uint16_t)i;
+    douts[i] = c.d_out + (uint64_t)i * L;
+    parts.push_back({outs[i], c.h_out + (uint64_t)i * L, L});
   }
+  rc = encode_device(2, k, ids.data(), n, c.d_in, size, size, 1, douts.data(), 0, 0, c.stream);
+  if (rc) return drained(rc);
+  hipError_t e = launch_sha256(c.d_out, L, L, n, c.d_out + dig, c.stream);  // save_temp's replica names (:79)
+  if (e != hipSuccess) return drained(hip_status(e));
+  e = launch_push(c.h_out_dev, c.d_out, dig + 32ull * n, c.stream);
+  if (e != hipSuccess) return drained(hip_status(e));
+  parts.push_back({replica_digests, c.h_out + dig, 32ull * n});
   // upload_data's hash of the body (server_api.cpp:16) on this thread while
   // the device works: one sequential chain, ~3 us a block in a GPU lane
   // (sha256_host.cpp)
   sha256_host(data, size, data_digest);
-  if (n) {
-    if ((rc = hip_status(hipStreamSynchronize(c.stream)))) return rc;
-    parallel_copy(parts);
-  }
+  if ((rc = hip_status(hipStreamSynchronize(c.stream)))) return rc;
+  parallel_copy(parts);
   return VDS_EC_OK;
 }
 

@@ -75,29 +75,23 @@ constexpr size_t kJitMaxEntries = 256;  // distinct survivor sets kept (never ev
 // are issued before the previous block's XORs.  k = 16, no spills up to 3
 // with prefetch (4 spilled 91 VGPRs) and 4 without; same-box repair, 512 x
 // 64 MiB: 2 14.62-14.72 ms, 3 14.52-14.60, 4 without prefetch 14.62
-// (profiles/round3/ab/jit_knobs.log).  VDS_EC_JIT_PB / VDS_EC_JIT_NOPF
-// override them (A/B).
-int fill_block() {
-  static const int pb = [] {
-    const char *v = std::getenv("VDS_EC_JIT_PB");
-    const int x = v ? std::atoi(v) : 0;
-    return x > 0 && x <= 32 ? x : 3;
-  }();
-  return pb;
-}
+// (profiles/round3/ab/jit_knobs.log).  -DVDS_JIT_PB=n / -DVDS_JIT_PREFETCH=0
+// builds override them (A/B).
+#ifndef VDS_JIT_PB
+#define VDS_JIT_PB 3
+#endif
+#ifndef VDS_JIT_PREFETCH
+#define VDS_JIT_PREFETCH 1
+#endif
+static_assert(VDS_JIT_PB > 0 && VDS_JIT_PB <= 32, "fill block size");
+constexpr int fill_block() { return VDS_JIT_PB; }
+constexpr bool fill_prefetch() { return VDS_JIT_PREFETCH != 0; }
 // Column-partitioned fill programs (xorprog.hpp emit_fill_scatter; default)
-// or the row form; VDS_EC_JIT_SCATTER=0 selects the row form (A/B).
-bool fill_scatter() {
-  static const bool sc = [] {
-    const char *v = std::getenv("VDS_EC_JIT_SCATTER");
-    return !(v && v[0] == '0');
-  }();
-  return sc;
-}
-bool fill_prefetch() {
-  static const bool pf = std::getenv("VDS_EC_JIT_NOPF") == nullptr;
-  return pf;
-}
+// or the row form (a -DVDS_JIT_SCATTER=0 build, A/B).
+#ifndef VDS_JIT_SCATTER
+#define VDS_JIT_SCATTER 1
+#endif
+constexpr bool fill_scatter() { return VDS_JIT_SCATTER != 0; }
 
 // JIT policy: 0 = off, 1 = background compile from a set's second use
 // (default), 2 = compile on the calling thread at the first use.  Initially
@@ -357,26 +351,37 @@ bool compile(const Key &key, std::vector<char> &code, std::string &log, std::str
       ok = !code.empty();
     }
   }
-  // VDS_EC_JIT_DUMP=<dir>: keep the source and code object (inspection)
-  if (const char *dump = std::getenv("VDS_EC_JIT_DUMP")) {
-    char base[512];
-    std::snprintf(base, sizeof base, "%s/jit_%u_%u_%llx%s", dump, key.k, key.n, (unsigned long long)key.survivors,
-                  key.regen ? "_regen" : "");
-    if (FILE *f = std::fopen((std::string(base) + ".hip").c_str(), "w")) {
-      std::fwrite(src.data(), 1, src.size(), f);
-      std::fclose(f);
-    }
-    if (ok)
-      if (FILE *f = std::fopen((std::string(base) + ".co").c_str(), "wb")) {
-        std::fwrite(code.data(), 1, code.size(), f);
-        std::fclose(f);
-      }
-  }
   std::remove(in.c_str());
   std::remove(out.c_str());
   std::remove(err.c_str());
   rmdir(dir.c_str());
   if (ok && !cached.empty()) cache_write(cached, ckey, code);  // (best effort)
+  return ok;
+}
+
+// vds_ec_jit_dump16: the set's source and code object under `dir`.
+bool dump(const Key &key, const char *dir) {
+  std::vector<char> code;
+  std::string log;
+  if (!compile(key, code, log)) {
+    std::fprintf(stderr, "vds_ec jit: compile failed:\n%s\n", log.c_str());
+    return false;
+  }
+  const std::string src = kernel_source(key);
+  char base[512];
+  std::snprintf(base, sizeof base, "%s/jit_%u_%u_%llx%s", dir, key.k, key.n, (unsigned long long)key.survivors,
+                key.regen ? "_regen" : "");
+  bool ok = false;
+  if (FILE *f = std::fopen((std::string(base) + ".hip").c_str(), "w")) {
+    ok = std::fwrite(src.data(), 1, src.size(), f) == src.size();
+    ok = (std::fclose(f) == 0) && ok;
+  }
+  if (FILE *f = std::fopen((std::string(base) + ".co").c_str(), "wb")) {
+    ok = (std::fwrite(code.data(), 1, code.size(), f) == code.size()) && ok;
+    ok = (std::fclose(f) == 0) && ok;
+  } else {
+    ok = false;
+  }
   return ok;
 }
 
@@ -609,6 +614,13 @@ int vds_ec_jit_ready16(uint16_t k, const uint16_t *nodes) {
   Key key;
   if (jit_key(k, nodes, &key)) return 0;
   return Jit::get().ready(key) ? 1 : 0;
+}
+
+int vds_ec_jit_dump16(uint16_t k, const uint16_t *nodes, int regen, const char *dir) {
+  Key key;
+  if (!dir || jit_key(k, nodes, &key)) return VDS_EC_EINVAL;
+  key.regen = regen ? 1u : 0u;
+  return dump(key, dir) ? VDS_EC_OK : VDS_EC_EHIP;
 }
 
 }  // extern "C"

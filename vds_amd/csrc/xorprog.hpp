@@ -375,15 +375,18 @@ inline size_t emit_fill_programs(std::string &s, const char *name, int K, const 
 // a quarter of its LDS reads.  Programs cover at most kScatterPart erased
 // points each (register pressure).
 constexpr int kScatterPart = 4;
-// survivors per Paar block of a scatter program (VDS_EC_JIT_SPB overrides).
+// survivors per Paar block of a scatter program (-DVDS_JIT_SPB=n overrides).
 // 2 spills 5-7 VGPRs and is still the fastest: same box, three rounds, k=16
 // repair 14.13-14.24 ms (2) vs 14.29-14.63 (1) vs 14.43-14.50 (row form);
 // 3 or 4 spill 66-174 (profiles/round3/ab/scatter_ab.log).
-inline int scatter_block() {
-  const char *v = std::getenv("VDS_EC_JIT_SPB");
-  const int x = v ? std::atoi(v) : 0;
-  return x >= 1 && x <= 4 ? x : 2;
-}
+#ifndef VDS_JIT_SPB
+#define VDS_JIT_SPB 2
+#endif
+#ifndef VDS_JIT_SPREFETCH
+#define VDS_JIT_SPREFETCH 1  // (a block's LDS reads issued before the previous block's XORs)
+#endif
+static_assert(VDS_JIT_SPB >= 1 && VDS_JIT_SPB <= 4, "scatter block size");
+constexpr int scatter_block() { return VDS_JIT_SPB; }
 // `targets` (optional): the points to compute instead of the erased points
 // below K -- the regenerate kernel's targets, every erased point of 0..N-1.
 inline size_t emit_fill_scatter(std::string &s, const char *name, int K, const std::vector<int> &spoints,
@@ -435,7 +438,7 @@ inline size_t emit_fill_scatter(std::string &s, const char *name, int K, const s
       InputMap im;  // (this wave's survivors, in their own LDS slots)
       for (int i = 0; i < 4; ++i) im.map.push_back(spoints[4 * w + i]);
       total += emit_program(s, nm, sub, 4, row_range(0, (int)sub.size()), scatter_block(), im,
-                            std::getenv("VDS_EC_JIT_SNOPF") == nullptr);
+                            VDS_JIT_SPREFETCH != 0);
     }
   for (int q = 0; q < parts; ++q) {
     appendf(s, "  template <typename In>\n  __device__ __forceinline__ static void fill_part%d(int w, const In &IN4, uint32_t (&acc)[%d]) {\n",

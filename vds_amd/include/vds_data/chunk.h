@@ -11,8 +11,10 @@
 //  * chunk_restore with repeated replica ids: the reference computes garbage
 //    (its validation is vds_assert, compiled out); here restore() returns an
 //    error and multipliers() is all-zero.
-//  * chunk_generator is move-only (the reference's implicit copy would
-//    double-free multipliers_).
+//  * chunk_generator and chunk_restore are neither copyable nor movable (the
+//    copy operations are deleted; the reference's implicit copy would
+//    double-free multipliers_).  Every caller holds them by unique_ptr or as
+//    a local, which compiles unchanged.
 #ifndef __VDS_DATA_CHUNK_H_
 #define __VDS_DATA_CHUNK_H_
 

@@ -23,7 +23,7 @@ namespace api {
 // again.  (Bounded: past kMax entries the store is cleared.)
 struct SynPlanStore {
   static constexpr size_t kMax = 1u << 16;
-  std::mutex mu;
+  std::shared_mutex mu;  // (the batch planners look plans up from several threads at once)
   std::unordered_map<uint64_t, SynBatchPlan> map;
 };
 
@@ -85,21 +85,16 @@ bool small_plan_solve(uint32_t k, uint32_t ms, uint64_t seen, SynBatchPlan &p) {
   return true;
 }
 
-// The plan of the erased set ~seen (k, n = k + k/4 compiled; or, ms > 0, the
-// SMALL plan over 0..k+ms-1): points and erased points ascending, the solve
-// from the store or computed.
-bool syn_plan(uint32_t k, uint32_t n, uint64_t seen, SynBatchPlan *out, uint32_t ms) {
+// The store key of the erased set ~seen (k, n = k + k/4 compiled; or, ms >
+// 0, the SMALL plan over 0..k+ms-1).
+inline uint64_t syn_plan_key(uint32_t k, uint32_t n, uint64_t seen, uint32_t ms) {
   if (ms) n = k + ms;
-  const uint64_t key = (~seen & ((1ull << n) - 1)) | ((uint64_t)k << 56) | ((uint64_t)ms << 48);
-  SynPlanStore &st = syn_plan_store();
-  {
-    std::lock_guard<std::mutex> g(st.mu);
-    auto it = st.map.find(key);
-    if (it != st.map.end()) {
-      *out = it->second;
-      return true;
-    }
-  }
+  return (~seen & ((1ull << n) - 1)) | ((uint64_t)k << 56) | ((uint64_t)ms << 48);
+}
+
+// Solve the plan of that set: points and erased points ascending, the M x M
+// solve as bit selections (or SMALL's masks).  No store access.
+bool syn_plan_solve(uint32_t k, uint32_t n, uint64_t seen, SynBatchPlan *out, uint32_t ms) {
   SynBatchPlan p{};
   if (ms) {
     if (!small_plan_solve(k, ms, seen, p)) return false;
@@ -117,9 +112,6 @@ bool syn_plan(uint32_t k, uint32_t n, uint64_t seen, SynBatchPlan *out, uint32_t
     std::memcpy(p.point, sa.point, sizeof p.point);
     std::memcpy(p.solve_sel, sa.solve_sel, sizeof p.solve_sel);
   }
-  std::lock_guard<std::mutex> g(st.mu);
-  if (st.map.size() >= SynPlanStore::kMax) st.map.clear();
-  st.map.emplace(key, p);
   *out = p;
   return true;
 }
@@ -202,13 +194,19 @@ class HostPool {
   unsigned nworkers_ = 0;
 };
 
-// fn(o0, o1) over [0, count) in ranges of at least kMinPer objects.
-template <class F>
-void parallel_objects(uint32_t count, F &&fn) {
+// fn(part, o0, o1) over [0, count) in at most kMaxParts contiguous ranges of
+// at least kMinPer objects; a call with the same count always makes the same
+// ranges, so a later pass can continue from per-part totals of an earlier one.
+constexpr unsigned kMaxParts = 8;
+inline unsigned batch_parts(uint32_t count) {
   constexpr uint32_t kMinPer = 1024;
-  const unsigned parts = std::min<uint32_t>(8, std::max<uint32_t>(1, count / kMinPer));
+  return std::min<uint32_t>(kMaxParts, std::max<uint32_t>(1, count / kMinPer));
+}
+template <class F>
+void parallel_parts(uint32_t count, F &&fn) {
+  const unsigned parts = batch_parts(count);
   HostPool::get().run(parts, [&](unsigned p) {
-    fn((uint32_t)((uint64_t)count * p / parts), (uint32_t)((uint64_t)count * (p + 1) / parts));
+    fn(p, (uint32_t)((uint64_t)count * p / parts), (uint32_t)((uint64_t)count * (p + 1) / parts));
   });
 }
 
@@ -241,6 +239,7 @@ struct BatchObjInfo {
   uint8_t parts;    // RT descriptors (regenerate: rows in groups of at most n - k)
   uint8_t ms;       // kRouteSyn: SMALL ms (1, 2) over 0..k+ms-1, kMsPerm, or 0 = the N = k + k/4 kernel
   uint16_t target;  // kMsPerm: the one target
+  uint32_t plan;    // kRouteSyn: its plan's claim number (SynBatchBuild::plan_of)
 };
 
 // (BatchObjInfo::ms of the PERM regenerate: survivors exactly 0..k-1, one
@@ -284,108 +283,198 @@ inline bool id_set(uint32_t k, const uint16_t *nd, uint64_t *seen, uint32_t *max
 
 // Host-side builder of one k_restore_syn batch launch, written straight into
 // a pinned parameter slot: objs (and the empty object), then tiles, then
-// plans.  plan_of() (serial) resolves survivor sets to plans; fill() writes
-// descriptor i and may run on several threads for distinct i.
+// plans.  plan_of() resolves survivor sets to plans and fill() writes
+// descriptor i; both run on several threads at once (distinct i).
+//
+// Plans by class (rank: SMALL ms = 1, ms = 2, PERM, the N = k + k/4 syndrome
+// kernel's), each class's plans contiguous in the slot so its tiles are too.
+// In the first pass the first object of a new set claims it in a call-wide
+// hash (CAS) and numbers it within its own (class, part) region, so the
+// parts share no counter; numbered() then maps a claim to its dense slot
+// index (class, then part, then claim order) in O(1).  In the second pass
+// each part first fills the plans it claimed -- from the process-wide store
+// under one lock hold, solving what the store lacks -- and then writes its
+// descriptors with dense plan numbers.  (Claims through a shared counter and
+// per-set store locking from eight threads made that pass 4x slower.)
+inline uint32_t plan_class_rank(uint32_t ms) { return ms == 1 ? 0 : ms == 2 ? 1 : ms == kMsPerm ? 2 : 3; }
 struct SynBatchBuild {
+  static constexpr uint32_t kPending = 0xFFFFFFFFu;
+  static constexpr int kRegionShift = 27;  // claim = (class * kMaxParts + part) << 27 | index within the region
   uint32_t k, n;
   bool regen = false;
-  // plans [0, cls_end[0]) are SMALL ms = 1, [cls_end[0], cls_end[1]) ms = 2,
-  // [cls_end[1], cls_end[2]) PERM, the rest the N = k + k/4 syndrome
-  // kernel's (batch_begin resolves them in that order); each class is one
-  // launch over its plans' tiles
-  uint32_t cls_end[3] = {0, 0, 0};
-  uint32_t perm_idx[64];  // PERM plan of target t (k <= t < 2k), or UINT32_MAX
   ParamSlot *slot = nullptr;
-  size_t cap_objs = 0, cap_tiles = 0, cap_plans = 0, o_tiles = 0, o_plans = 0;
+  size_t cap_objs = 0, cap_tiles = 0, o_tiles = 0, o_plans = 0;
   SynBatchObj *objs = nullptr;
   uint32_t nobj = 0;
   std::vector<uint32_t> obj_plan, obj_halves;
-  std::vector<SynBatchPlan> plans;
-  // survivor set -> plans[]: open addressing, linear probing (a set is a
-  // nonzero bitmask; 0 marks a free entry)
-  std::vector<uint64_t> hkey;
-  std::vector<uint32_t> hval;
-  std::vector<uint32_t> hused;  // entries of hkey in use (cleared one by one when the table is reused)
+  struct PlanReq {
+    uint64_t seen;
+    uint32_t claim;
+    uint8_t ms;
+    uint16_t target;
+  };
+  struct alignas(64) PartPlans {  // (one cache line apart: the parts write them concurrently)
+    std::vector<uint32_t> hused;  // table entries this part claimed (cleared one by one when the table is reused)
+    std::vector<PlanReq> reqs, miss;
+    uint32_t next[4];  // claims in each class
+  };
+  PartPlans pp[kMaxParts];
+  uint32_t dense[4 * kMaxParts + 1];   // first slot plan of each (class, part) region
+  uint32_t cls_end[4] = {0, 0, 0, 0};  // dense class ranges: [cls_end[c - 1], cls_end[c])
+  // (survivor set, ms, PERM target) -> claim: open addressing, linear
+  // probing, filled concurrently (a key is taken by CAS; its value reads
+  // kPending until the claimer has numbered it)
+  struct Entry {  // key and claim in one 16-byte entry: a claim moves one cache line between cores, not two
+    uint64_t key;
+    uint32_t val;
+    uint32_t pad;
+  };
+  std::vector<Entry> ht;
   std::vector<uint64_t> first_, used_;
-  std::vector<SynBatchPlan> sorted_;  // (batch_begin's class order; swapped with plans)
   unsigned hshift = 64;
 
   static size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
 
   // A builder is per thread and reused (batch_scratch): the vectors keep
-  // their capacity, so a steady stream of calls allocates nothing.
-  void reset(uint32_t k_, uint32_t n_) {
+  // their capacity, so a steady stream of calls allocates nothing.  The
+  // claim table is made ready for `count` objects.
+  void reset(uint32_t k_, uint32_t n_, uint32_t count) {
     k = k_;
     n = n_;
     regen = false;
-    cls_end[0] = cls_end[1] = cls_end[2] = 0;
     slot = nullptr;
-    cap_objs = cap_tiles = cap_plans = o_tiles = o_plans = 0;
+    cap_objs = cap_tiles = o_tiles = o_plans = 0;
     objs = nullptr;
     nobj = 0;
-    plans.clear();
+    unsigned bits = 4;
+    while ((1ull << bits) < 2ull * count) ++bits;
+    if (ht.size() != (1ull << bits)) {
+      ht.assign(1ull << bits, Entry{0, kPending, 0});
+      for (PartPlans &q : pp) q.hused.clear();
+    }
+    for (PartPlans &q : pp) {
+      for (const uint32_t x : q.hused) {
+        ht[x].key = 0;
+        ht[x].val = kPending;
+      }
+      q.hused.clear();
+      q.reqs.clear();
+      for (uint32_t &x : q.next) x = 0;
+    }
+    hshift = 64 - bits;
+  }
+  // The claim of survivor set `seen` (ms > 0: the SMALL plan over 0..k+ms-1,
+  // or kMsPerm: survivors 0..k-1 and one target in k..2k-1; a set always
+  // resolves to the same ms within a call: the route is a function of the
+  // set), taken on first sight.  Thread-safe across parts (part: the
+  // caller's parallel_parts range).
+  uint32_t plan_of(unsigned part, uint64_t seen, uint32_t ms, uint32_t target) {
+    // (keyed by set AND ms: a regenerate's route also depends on its targets,
+    // so one set may meet two SMALL sizes in a call; PERM also by target)
+    const uint64_t hk = seen | ((uint64_t)ms << 56) | (ms == kMsPerm ? (uint64_t)target << 48 : 0);
+    const size_t mask = ht.size() - 1;
+    size_t i = (size_t)((hk * 0x9E3779B97F4A7C15ull) >> hshift);
+    for (;;) {
+      uint64_t cur = __atomic_load_n(&ht[i].key, __ATOMIC_ACQUIRE);
+      if (cur == 0) {
+        if (__atomic_compare_exchange_n(&ht[i].key, &cur, hk, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+          PartPlans &q = pp[part];
+          const uint32_t c = plan_class_rank(ms);
+          const uint32_t v = ((c * kMaxParts + part) << kRegionShift) | q.next[c]++;
+          __atomic_store_n(&ht[i].val, v, __ATOMIC_RELEASE);
+          q.hused.push_back((uint32_t)i);
+          q.reqs.push_back(PlanReq{seen, v, (uint8_t)ms, (uint16_t)target});
+          return v;
+        }
+        // (another thread claimed the entry first: cur holds its key)
+      }
+      if (cur == hk) {
+        uint32_t v;
+        while ((v = __atomic_load_n(&ht[i].val, __ATOMIC_ACQUIRE)) == kPending) {
+        }  // (the claimer stores it right after numbering it)
+        return v;
+      }
+      i = (i + 1) & mask;
+    }
+  }
+  // After the first pass: the dense numbering of the claims.
+  uint32_t number_plans(unsigned parts) {
+    uint32_t at = 0;
+    for (int c = 0; c < 4; ++c) {
+      for (unsigned q = 0; q < kMaxParts; ++q) {
+        dense[c * kMaxParts + q] = at;
+        at += q < parts ? pp[q].next[c] : 0;
+      }
+      cls_end[c] = at;
+    }
+    dense[4 * kMaxParts] = at;
+    return at;
+  }
+  uint32_t numbered(uint32_t claim) const {
+    return dense[claim >> kRegionShift] + (claim & ((1u << kRegionShift) - 1));
+  }
+  // Part `part`'s claimed plans, into the slot (second pass, before its
+  // descriptors); false when a set has no solve (not for distinct points).
+  bool resolve_plans(unsigned part) {
+    PartPlans &q = pp[part];
+    SynBatchPlan *dst = reinterpret_cast<SynBatchPlan *>(slot->h + o_plans);
+    SynPlanStore &st = syn_plan_store();
+    bool ok = true;
+    q.miss.clear();
+    if (!q.reqs.empty()) {
+      std::shared_lock<std::shared_mutex> g(st.mu);
+      for (const PlanReq &r : q.reqs) {
+        if (r.ms == kMsPerm) continue;
+        auto it = st.map.find(syn_plan_key(k, n, r.seen, r.ms));
+        if (it != st.map.end())
+          dst[numbered(r.claim)] = it->second;
+        else
+          q.miss.push_back(r);
+      }
+    }
+    size_t solved = 0;
+    for (const PlanReq &r : q.miss) {
+      if (syn_plan_solve(k, n, r.seen, &dst[numbered(r.claim)], r.ms))
+        q.miss[solved++] = r;
+      else
+        ok = false;
+    }
+    if (solved) {
+      std::unique_lock<std::shared_mutex> g(st.mu);
+      if (st.map.size() + solved > SynPlanStore::kMax) st.map.clear();
+      for (size_t x = 0; x < solved; ++x)
+        st.map.emplace(syn_plan_key(k, n, q.miss[x].seen, q.miss[x].ms), dst[numbered(q.miss[x].claim)]);
+    }
+    for (const PlanReq &r : q.reqs) {
+      SynBatchPlan &pl = dst[numbered(r.claim)];
+      if (r.ms == kMsPerm) {
+        pl = SynBatchPlan{};
+        for (uint32_t j = 0; j < k; ++j) pl.point[j] = (uint8_t)j;
+        for (uint32_t e = 0; e < kMaxFastK / 4; ++e) pl.erased[e] = (uint8_t)r.target;
+        pl.cls = 3;  // (kClsPerm)
+      } else {
+        if (r.ms && regen) pl.nrec = r.ms;  // (regenerate: every erased point of A is a target candidate)
+        pl.cls = r.ms;                      // (kClsSyn = 0, kClsSmall1 / 2 = ms)
+      }
+    }
+    return ok;
   }
 
-  // The slot bytes for `count` objects of `halves` half tiles; then attach().
-  size_t layout(uint32_t count, uint64_t halves) {
+  // The slot bytes for `count` objects of `halves` half tiles and `plans`
+  // distinct plans; then attach().
+  size_t layout(uint32_t count, uint64_t halves, uint32_t plans) {
     nobj = count;
     cap_objs = (size_t)count + 1;
     cap_tiles = (size_t)((halves + count + 1) / 2 + 1);  // pairs within each plan: <= (halves + plans) / 2
-    cap_plans = count;
     o_tiles = up16(cap_objs * sizeof(SynBatchObj));
     o_plans = up16(o_tiles + cap_tiles * sizeof(SynBatchTile));
-    return o_plans + cap_plans * sizeof(SynBatchPlan);
+    return o_plans + (size_t)plans * sizeof(SynBatchPlan);
   }
   void attach(ParamSlot *sl) {
     slot = sl;
     objs = reinterpret_cast<SynBatchObj *>(slot->h);
-    const uint32_t count = nobj;
-    obj_plan.assign(count, 0);
-    obj_halves.assign(count, 0);
-    unsigned bits = 4;
-    while ((1ull << bits) < 2ull * count) ++bits;
-    if (hkey.size() != (1ull << bits)) {
-      hkey.assign(1ull << bits, 0);
-      hval.assign(1ull << bits, 0);
-    } else {
-      for (const uint32_t x : hused) hkey[x] = 0;
-    }
-    hused.clear();
-    hshift = 64 - bits;
-    for (uint32_t &x : perm_idx) x = UINT32_MAX;
-  }
-  // The plan of survivor set `seen` (UINT32_MAX: no solve; not for distinct
-  // points); ms > 0: the SMALL plan over 0..k+ms-1 (a set always resolves to
-  // the same ms within a call: the route is a function of the set).
-  uint32_t plan_of(uint64_t seen, uint32_t ms = 0, uint32_t target = 0) {
-    if (ms == kMsPerm) {  // survivors 0..k-1, one target t in k..2k-1: a plan per t
-      if (target < k || target >= 2 * k || target >= 64) return UINT32_MAX;
-      if (perm_idx[target] != UINT32_MAX) return perm_idx[target];
-      SynBatchPlan pl{};
-      for (uint32_t j = 0; j < k; ++j) pl.point[j] = (uint8_t)j;
-      for (uint32_t i = 0; i < kMaxFastK / 4; ++i) pl.erased[i] = (uint8_t)target;
-      pl.cls = 3;  // (kClsPerm)
-      perm_idx[target] = (uint32_t)plans.size();
-      plans.push_back(pl);
-      return perm_idx[target];
-    }
-    // (keyed by set AND ms: a regenerate's route also depends on its targets,
-    // so one set may meet two SMALL sizes in a call)
-    const uint64_t hk = seen | ((uint64_t)ms << 56);
-    const size_t mask = hkey.size() - 1;
-    size_t i = (size_t)((hk * 0x9E3779B97F4A7C15ull) >> hshift);
-    while (hkey[i] != 0 && hkey[i] != hk) i = (i + 1) & mask;
-    if (hkey[i] == hk) return hval[i];
-    SynBatchPlan pl;
-    if (!syn_plan(k, n, seen, &pl, ms)) return UINT32_MAX;
-    if (ms && regen) pl.nrec = ms;  // (regenerate: every erased point of A is a target candidate)
-    pl.cls = ms;                    // (kClsSyn = 0, kClsSmall1 / 2 = ms)
-    const uint32_t p = (uint32_t)plans.size();
-    plans.push_back(pl);
-    hkey[i] = hk;
-    hval[i] = p;
-    hused.push_back((uint32_t)i);
-    return p;
+    obj_plan.resize(nobj);
+    obj_halves.resize(nobj);
   }
   // Descriptor i: survivors in the plan's point order (ascending ids).
   SynBatchObj &fill(uint32_t i, uint64_t seen, const uint16_t *nd, const uint8_t *const *chunks, uint32_t plan,
@@ -411,20 +500,22 @@ struct SynBatchBuild {
     if (nobj == 0) return hip_status(param_release(slot, s));
     const uint32_t empty = nobj;
     std::memset(&objs[empty], 0, sizeof(SynBatchObj));
+    const uint32_t np = cls_end[3];
+    const uint32_t base[5] = {0, cls_end[0], cls_end[1], cls_end[2], cls_end[3]};
     std::vector<uint64_t> &first = first_, &used = used_;
-    first.assign(plans.size() + 1, 0);  // tile offset of each plan
-    used.assign(plans.size(), 0);
+    first.assign(np + 1, 0);  // tile offset of each plan
+    used.assign(np, 0);
     for (uint32_t o = 0; o < nobj; ++o) first[obj_plan[o] + 1] += obj_halves[o];
-    for (size_t p = 0; p < plans.size(); ++p) first[p + 1] = first[p] + (first[p + 1] + 1) / 2;
-    const uint64_t ntiles = first[plans.size()];
+    for (size_t p = 0; p < np; ++p) first[p + 1] = first[p] + (first[p + 1] + 1) / 2;
+    const uint64_t ntiles = first[np];
     if (ntiles > cap_tiles || ntiles > 0xFFFFFFFFull) {
       (void)param_release(slot, s);
       return VDS_EC_EINVAL;
     }
-    // classes (plans resolved class by class: contiguous plan and tile ranges)
-    const uint32_t bound[4] = {cls_end[0], cls_end[1], cls_end[2], (uint32_t)plans.size()};
+    // classes (contiguous plan and tile ranges)
+    const uint32_t *bound = base + 1;
     int ncls = 0;
-    for (int c = 0, q0 = 0; c < 4; q0 = bound[c], ++c) ncls += first[bound[c]] > first[q0];
+    for (int c = 0; c < 4; ++c) ncls += first[base[c + 1]] > first[base[c]];
     // MULTI (ncls > 1): tile t goes to position pos(t), so that each XCD's
     // contiguous eighth of the launch (tile_range) gets every eighth tile --
     // the same mix of classes, whose tiles cost differently
@@ -435,7 +526,7 @@ struct SynBatchBuild {
       return r * (R / 8) + std::min<uint64_t>(r, R % 8) + t / 8;
     };
     SynBatchTile *tiles = reinterpret_cast<SynBatchTile *>(slot->h + o_tiles);
-    for (size_t p = 0; p < plans.size(); ++p)
+    for (size_t p = 0; p < np; ++p)
       for (uint64_t t = first[p]; t < first[p + 1]; ++t)
         tiles[pos(t)] = SynBatchTile{{empty, empty}, {0, 0}, (uint32_t)p, 0, 0, 0};
     for (uint32_t o = 0; o < nobj; ++o) {
@@ -448,8 +539,7 @@ struct SynBatchBuild {
         if (regen && h + 1 == obj_halves[o]) t.trailer |= 1u << (i & 1);
       }
     }
-    std::memcpy(slot->h + o_plans, plans.data(), plans.size() * sizeof(SynBatchPlan));
-    hipError_t e = param_commit(slot, o_plans + plans.size() * sizeof(SynBatchPlan), s);
+    hipError_t e = param_commit(slot, o_plans + (size_t)np * sizeof(SynBatchPlan), s);
     if (e == hipSuccess) {
       SynRestoreArgs sa{};
       sa.objs = reinterpret_cast<const SynBatchObj *>(slot->d);
@@ -635,32 +725,44 @@ struct RtBatchBuild {
   }
 };
 
-// Prefix indices of the routed objects: syn[o] / rt[o] = descriptor index,
-// rtrow[o] = first coefficient row; counts and half / row totals.
-struct BatchIndex {
-  std::vector<uint32_t> syn, rt;
-  std::vector<uint64_t> rtrow;
+// Totals of the routed objects per part of a batch call (parallel_parts
+// ranges): counted by the first pass, prefix-summed, then each part of the
+// second pass numbers its own objects' descriptors and rows from its base.
+struct PartTotals {
   uint32_t nsyn = 0, nrt = 0;
   uint64_t syn_halves = 0, rt_halves = 0, rt_rows = 0;
-  void build(const std::vector<BatchObjInfo> &info) {
-    const uint32_t count = (uint32_t)info.size();
-    nsyn = nrt = 0;
-    syn_halves = rt_halves = rt_rows = 0;
-    syn.assign(count, 0);
-    rt.assign(count, 0);
-    rtrow.assign(count, 0);
-    for (uint32_t o = 0; o < count; ++o) {
-      const BatchObjInfo &f = info[o];
-      if (f.route == kRouteSyn) {
-        syn[o] = nsyn++;
-        syn_halves += f.halves;
-      } else if (f.route == kRouteRt) {
-        rt[o] = nrt;
-        rtrow[o] = rt_rows;
-        nrt += f.parts;
-        rt_halves += (uint64_t)f.parts * f.halves;
-        rt_rows += f.rows;
-      }
+  void add(const BatchObjInfo &f) {
+    if (f.route == kRouteSyn) {
+      ++nsyn;
+      syn_halves += f.halves;
+    } else if (f.route == kRouteRt) {
+      nrt += f.parts;
+      rt_halves += (uint64_t)f.parts * f.halves;
+      rt_rows += f.rows;
+    }
+  }
+  void add(const PartTotals &t) {
+    nsyn += t.nsyn;
+    nrt += t.nrt;
+    syn_halves += t.syn_halves;
+    rt_halves += t.rt_halves;
+    rt_rows += t.rt_rows;
+  }
+};
+struct BatchIndex {
+  PartTotals part[kMaxParts];  // the first pass's totals of each part
+  PartTotals base[kMaxParts];  // each part's first descriptor / row (build())
+  PartTotals all;
+  unsigned parts = 0;
+  void reset(uint32_t count) {
+    parts = batch_parts(count);
+    for (PartTotals &t : part) t = PartTotals{};
+  }
+  void build() {
+    all = PartTotals{};
+    for (unsigned p = 0; p < parts; ++p) {
+      base[p] = all;
+      all.add(part[p]);
     }
   }
 };
@@ -694,15 +796,12 @@ struct HostTrace {
   }
 };
 
-// Acquire both builders' slots (together: see param_acquire_n), resolve the
-// syndrome objects' plans (serial: the plan store and the per-call hash).
 // The batch calls' per-object tables, per thread and reused: at 16K objects
 // a call's fresh vectors came from mmap and paid their page faults every
 // call (~100 us of the planning at loss 0.25).
 struct BatchScratch {
   std::vector<uint64_t> lens;
   std::vector<BatchObjInfo> info;
-  std::vector<uint32_t> plan;
   BatchIndex ix;
   SynBatchBuild bb;
   RtBatchBuild rb;
@@ -712,66 +811,35 @@ BatchScratch &batch_scratch() {
   return sc;
 }
 
-int batch_begin(const std::vector<BatchObjInfo> &info, const BatchIndex &ix, SynBatchBuild &bb, RtBatchBuild &rb,
-                std::vector<uint32_t> &plan, hipStream_t s, HostTrace *ht) {
+// Acquire both builders' slots (together: see param_acquire_n).
+int batch_begin(const BatchIndex &ix, SynBatchBuild &bb, RtBatchBuild &rb, HostTrace *ht) {
   size_t bytes[2];
   ParamSlot *sl[2] = {};
   int nb = 0;
-  if (ix.nsyn) bytes[nb++] = bb.layout(ix.nsyn, ix.syn_halves);
-  if (ix.nrt) bytes[nb++] = rb.layout(ix.nrt, ix.rt_halves, ix.rt_rows);
+  if (ix.all.nsyn) bytes[nb++] = bb.layout(ix.all.nsyn, ix.all.syn_halves, bb.number_plans(ix.parts));
+  if (ix.all.nrt) bytes[nb++] = rb.layout(ix.all.nrt, ix.all.rt_halves, ix.all.rt_rows);
   const hipError_t e = param_acquire_n(nb, bytes, sl);
   if (e != hipSuccess) return hip_status(e);
   if (ht) ht->mark("acquire");
   nb = 0;
-  if (ix.nsyn) bb.attach(sl[nb++]);
-  if (ix.nrt) rb.attach(sl[nb++]);
+  if (ix.all.nsyn) bb.attach(sl[nb++]);
+  if (ix.all.nrt) rb.attach(sl[nb++]);
   if (ht) ht->mark("attach");
-  if (ix.nsyn) {
-    // One pass resolves every object's plan (first seen, first numbered);
-    // then the plans are renumbered class by class -- SMALL ms = 1, ms = 2,
-    // PERM, the N = k + k/4 kernel's (SynBatchBuild::cls_end) -- so each
-    // class's tiles are contiguous.  (Four passes, one per class, cost ~30 us
-    // more at 16K objects; finding the distinct sets in parallel and
-    // resolving each once measured slower still: 110 -> 245 us.)
-    const uint32_t count = (uint32_t)info.size();
-    plan.assign(count, 0);
-    for (uint32_t o = 0; o < count; ++o)
-      if (info[o].route == kRouteSyn &&
-          (plan[o] = bb.plan_of(info[o].seen, info[o].ms, info[o].target)) == UINT32_MAX) {
-        bb.abandon(s);
-        if (ix.nrt) rb.abandon(s);
-        return VDS_EC_ESINGULAR;
-      }
-    if (ht) ht->mark("plans");
-    const size_t np = bb.plans.size();
-    auto rank = [](uint32_t cls) { return cls == 1 ? 0 : cls == 2 ? 1 : cls == 3 ? 2 : 3; };
-    std::vector<uint32_t> order(np), remap(np);
-    uint32_t cnt[5] = {0, 0, 0, 0, 0};
-    for (size_t p = 0; p < np; ++p) ++cnt[rank(bb.plans[p].cls) + 1];
-    for (int c = 1; c < 5; ++c) cnt[c] += cnt[c - 1];
-    for (int c = 0; c < 3; ++c) bb.cls_end[c] = cnt[c + 1];
-    for (size_t p = 0; p < np; ++p) {
-      const uint32_t q = cnt[rank(bb.plans[p].cls)]++;
-      order[q] = (uint32_t)p;
-      remap[p] = q;
-    }
-    std::vector<SynBatchPlan> &sorted = bb.sorted_;
-    sorted.resize(np);
-    for (size_t q = 0; q < np; ++q) sorted[q] = bb.plans[order[q]];
-    bb.plans.swap(sorted);
-    for (uint32_t o = 0; o < count; ++o)
-      if (info[o].route == kRouteSyn) plan[o] = remap[plan[o]];
-  }
   return VDS_EC_OK;
 }
 
+void batch_abandon(const BatchIndex &ix, SynBatchBuild &bb, RtBatchBuild &rb, hipStream_t s) {
+  if (ix.all.nsyn) bb.abandon(s);
+  if (ix.all.nrt) rb.abandon(s);
+}
+
 int batch_launch(const BatchIndex &ix, SynBatchBuild &bb, RtBatchBuild &rb, bool regen, hipStream_t s) {
-  int rc = ix.nsyn ? bb.launch(regen, s) : VDS_EC_OK;
+  int rc = ix.all.nsyn ? bb.launch(regen, s) : VDS_EC_OK;
   if (rc) {
-    if (ix.nrt) rb.abandon(s);
+    if (ix.all.nrt) rb.abandon(s);
     return rc;
   }
-  return ix.nrt ? rb.launch(regen, s) : VDS_EC_OK;
+  return ix.all.nrt ? rb.launch(regen, s) : VDS_EC_OK;
 }
 
 int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
@@ -784,16 +852,22 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
   const bool syn = batch_ok && !restore_path_override_bs();
   HostTrace ht("restore_batch");
   // pass 1 (parallel): every object validated before anything is enqueued,
-  // its route and sizes
+  // its route and sizes; per-part totals
   BatchScratch &sc = batch_scratch();
   std::vector<uint64_t> &lens = sc.lens;
   std::vector<BatchObjInfo> &info = sc.info;
-  lens.assign(count, 0);
-  info.assign(count, BatchObjInfo{});
+  lens.resize(count);
+  info.resize(count);
+  BatchIndex &ix = sc.ix;
+  ix.reset(count);
+  SynBatchBuild &bb = sc.bb;
+  bb.reset(k, n, count);
   FirstError err;
-  parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
+  parallel_parts(count, [&](unsigned part, uint32_t o0, uint32_t o1) {
+    PartTotals tot;
     for (uint32_t o = o0; o < o1; ++o) {
       const uint16_t *nd = nodes + (uint64_t)o * k;
+      lens[o] = 0;
       int rc = check_restore_args(k, nd, chunks + (uint64_t)o * k, chunk_sizes[o]);
       bool ok = true;
       if (!rc) lens[o] = restored_len(2, k, chunk_sizes[o], paddings[o], flags, &ok);
@@ -804,6 +878,7 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
       if (!rc && lens[o] && !id_set(k, nd, &f.seen, &maxid)) rc = VDS_EC_ESINGULAR;
       if (rc) {
         err.note(o, rc);
+        info[o] = f;
         return;
       }
       const uint64_t need = (lens[o] + 2ull * k - 1) / (2ull * k);  // stripes that produce output
@@ -815,6 +890,7 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
       } else if (syn && fits && maxid < n) {
         f.route = kRouteSyn;
         f.ms = small_ms_for(k, maxid);
+        f.plan = bb.plan_of(part, f.seen, f.ms, 0);
       } else if (batch_ok && fits && maxid < 256) {
         f.route = kRouteRt;
         f.parts = 1;
@@ -823,37 +899,43 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
         f.route = kRouteOne;
       }
       info[o] = f;
+      tot.add(f);
     }
+    ix.part[part] = tot;
   });
   if (err.rc) return err.rc;
   int rc = device_ready();
   if (rc) return rc;
   ht.mark("pass1");
-  BatchIndex &ix = sc.ix;
-  ix.build(info);
-  SynBatchBuild &bb = sc.bb;
-  bb.reset(k, n);
+  ix.build();
   RtBatchBuild &rb = sc.rb;
   rb.reset(k, n);
   rb.rt2 = rt2_enabled();  // (restore only; RtBatchBuild::fill decides per object)
-  std::vector<uint32_t> &plan = sc.plan;
-  ht.mark("index");
-  if ((rc = batch_begin(info, ix, bb, rb, plan, s, &ht))) return rc;
+  if ((rc = batch_begin(ix, bb, rb, &ht))) return rc;
   ht.mark("begin");
-  // pass 2 (parallel): the descriptors
-  parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
+  // pass 2 (parallel): the plans (resolved here, concurrently) and the
+  // descriptors, numbered from each part's base
+  parallel_parts(count, [&](unsigned part, uint32_t o0, uint32_t o1) {
+    if (ix.all.nsyn && !bb.resolve_plans(part)) {  // (a set with no solve: not for distinct points)
+      err.note(o0, VDS_EC_ESINGULAR);
+      return;
+    }
+    uint32_t isyn = ix.base[part].nsyn, irt = ix.base[part].nrt;
+    uint64_t row = ix.base[part].rt_rows;
     for (uint32_t o = o0; o < o1; ++o) {
       const BatchObjInfo &f = info[o];
       const uint16_t *nd = nodes + (uint64_t)o * k;
       const uint8_t *const *ch = chunks + (uint64_t)o * k;
       SynBatchObj *d;
       if (f.route == kRouteSyn) {
-        d = &bb.fill(ix.syn[o], f.seen, nd, ch, plan[o], f.halves);
+        d = &bb.fill(isyn++, f.seen, nd, ch, bb.numbered(f.plan), f.halves);
       } else if (f.route == kRouteRt) {
         uint8_t rowp[kMaxFastK];
         uint32_t ne = 0;
         for (uint64_t b = ~f.seen & ((1ull << k) - 1); b; b &= b - 1) rowp[ne++] = (uint8_t)__builtin_ctzll(b);
-        d = &rb.fill(ix.rt[o], nd, ch, rowp, ne, ix.rtrow[o], f.halves);
+        d = &rb.fill(irt, nd, ch, rowp, ne, row, f.halves);
+        irt += f.parts;
+        row += f.rows;
       } else {
         continue;
       }
@@ -863,6 +945,10 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
       d->chunk_len = chunk_sizes[o];
     }
   });
+  if (err.rc) {
+    batch_abandon(ix, bb, rb, s);
+    return err.rc;
+  }
   ht.mark("pass2");
   if ((rc = batch_launch(ix, bb, rb, false, s))) return rc;
   ht.mark("launch");
@@ -894,9 +980,15 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
   HostTrace ht("regenerate_batch");
   BatchScratch &sc = batch_scratch();
   std::vector<BatchObjInfo> &info = sc.info;
-  info.assign(count, BatchObjInfo{});
+  info.resize(count);
+  BatchIndex &ix = sc.ix;
+  ix.reset(count);
+  SynBatchBuild &bb = sc.bb;
+  bb.reset(k, n, count);
+  bb.regen = true;
   FirstError err;
-  parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
+  parallel_parts(count, [&](unsigned part, uint32_t o0, uint32_t o1) {
+    PartTotals tot;
     for (uint32_t o = o0; o < o1; ++o) {
       const uint16_t *nd = nodes + (uint64_t)o * k;
       const uint16_t *tg = targets + (uint64_t)o * nt;
@@ -911,6 +1003,7 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
       if (!rc && !id_set(k, nd, &f.seen, &maxid)) rc = VDS_EC_ESINGULAR;
       if (rc) {
         err.note(o, rc);
+        info[o] = f;
         return;
       }
       const uint64_t T = (chunk_sizes[o] - 2) / 2;
@@ -933,37 +1026,45 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
         f.route = kRouteSyn;  // survivors exactly 0..k-1 (k distinct ids below k), one target in k..2k-1
         f.ms = kMsPerm;
         f.target = tg[0];
+        f.plan = bb.plan_of(part, f.seen, f.ms, f.target);
       } else if (ok) {
         f.route = kRouteSyn;
         f.ms = small_ms_for(k, std::max(maxid, tmax));  // (every target an erased point of 0..k+ms-1)
+        f.plan = bb.plan_of(part, f.seen, f.ms, 0);
       } else if (batch_ok && fits && maxid < 256 && tmax < 256) {
         f.route = kRouteRt;
         f.parts = (uint8_t)((nt + R - 1) / R);
         f.rows = (uint16_t)nt;
+        // (RT descriptors per object: nt / (n - k) rounded up, < 256)
+        if ((uint32_t)f.parts * R < nt) {
+          err.note(o, VDS_EC_EINVAL);
+          info[o] = BatchObjInfo{};
+          return;
+        }
       } else {
         f.route = kRouteOne;
       }
       info[o] = f;
+      tot.add(f);
     }
+    ix.part[part] = tot;
   });
   if (err.rc) return err.rc;
   int rc = device_ready();
   if (rc) return rc;
-  for (const BatchObjInfo &f : info)  // (RT descriptors per object: nt / (n - k) rounded up, < 256)
-    if (f.route == kRouteRt && (uint32_t)f.parts * R < nt) return VDS_EC_EINVAL;
   ht.mark("pass1");
-  BatchIndex &ix = sc.ix;
-  ix.build(info);
-  SynBatchBuild &bb = sc.bb;
-  bb.reset(k, n);
-  bb.regen = true;
+  ix.build();
   RtBatchBuild &rb = sc.rb;
   rb.reset(k, n);
-  std::vector<uint32_t> &plan = sc.plan;
-  ht.mark("index");
-  if ((rc = batch_begin(info, ix, bb, rb, plan, s, &ht))) return rc;
+  if ((rc = batch_begin(ix, bb, rb, &ht))) return rc;
   ht.mark("begin");
-  parallel_objects(count, [&](uint32_t o0, uint32_t o1) {
+  parallel_parts(count, [&](unsigned part, uint32_t o0, uint32_t o1) {
+    if (ix.all.nsyn && !bb.resolve_plans(part)) {  // (a set with no solve: not for distinct points)
+      err.note(o0, VDS_EC_ESINGULAR);
+      return;
+    }
+    uint32_t isyn = ix.base[part].nsyn, irt = ix.base[part].nrt;
+    uint64_t row = ix.base[part].rt_rows;
     for (uint32_t o = o0; o < o1; ++o) {
       const BatchObjInfo &f = info[o];
       const uint16_t *nd = nodes + (uint64_t)o * k;
@@ -971,7 +1072,7 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
       const uint16_t *tg = targets + (uint64_t)o * nt;
       uint8_t *const *os = outs + (uint64_t)o * nt;
       if (f.route == kRouteSyn) {
-        SynBatchObj &d = bb.fill(ix.syn[o], f.seen, nd, ch, plan[o], f.halves);
+        SynBatchObj &d = bb.fill(isyn++, f.seen, nd, ch, bb.numbered(f.plan), f.halves);
         std::memset(d.regen, 0, sizeof d.regen);
         if (f.ms == kMsPerm) {
           d.regen[0] = os[0];  // (the plan's erased[0] is the target)
@@ -985,20 +1086,26 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
         d.out_len = 0;
         d.chunk_len = chunk_sizes[o];
       } else if (f.route == kRouteRt) {
-        for (uint32_t part = 0, i0 = 0; part < f.parts; ++part, i0 += R) {
+        for (uint32_t p = 0, i0 = 0; p < f.parts; ++p, i0 += R) {
           const uint32_t cnt = std::min(R, nt - i0);
           uint8_t rowp[kMaxFastK / 4];
           for (uint32_t i = 0; i < cnt; ++i) rowp[i] = (uint8_t)tg[i0 + i];
-          SynBatchObj &d = rb.fill(ix.rt[o] + part, nd, ch, rowp, cnt, ix.rtrow[o] + i0, f.halves);
+          SynBatchObj &d = rb.fill(irt + p, nd, ch, rowp, cnt, row + i0, f.halves);
           std::memset(d.regen, 0, sizeof d.regen);
           for (uint32_t i = 0; i < cnt; ++i) d.regen[i] = os[i0 + i];
           d.out = nullptr;
           d.out_len = 0;
           d.chunk_len = chunk_sizes[o];
         }
+        irt += f.parts;
+        row += f.rows;
       }
     }
   });
+  if (err.rc) {
+    batch_abandon(ix, bb, rb, s);
+    return err.rc;
+  }
   ht.mark("pass2");
   if ((rc = batch_launch(ix, bb, rb, true, s))) return rc;
   ht.mark("launch");

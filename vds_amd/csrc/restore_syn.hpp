@@ -261,6 +261,17 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
   }
 }
 
+// S1's input with point EP served from registers (the own-group fill below).
+template <int EP>
+struct S1In {
+  const SynLds &L;
+  const Plane16 &own;
+  __device__ __forceinline__ u32x4 operator()(int g) const {
+    if ((g >> 2) == EP) return u32x4{own.p[4 * (g & 3)], own.p[4 * (g & 3) + 1], own.p[4 * (g & 3) + 2], own.p[4 * (g & 3) + 3]};
+    return L(g);
+  }
+};
+
 // Two-level interpolation (VDS_GM2, default; generated gm_* programs,
 // tools/xorgen/gen_restore.cpp emit_gm2): levels 1 and 2 of the additive FFT
 // on each wave's own four slots (S1, in place), the K/4-point direct
@@ -289,19 +300,25 @@ __device__ __forceinline__ void syn_interp_gm(int wave, const SynLds &L, uint32_
 #ifndef VDS_HALF_PRIO
 #define VDS_HALF_PRIO 1
 #endif
-template <int K, int N, int WV, int W, class Tail>
-__device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, Stamps &st, Tail &&tail) {
+// OwnP (not void): the own-group fill's policy; `own` is this wave's group's
+// erased point, which S1 takes from registers.
+template <int K, int N, int WV, int W, class Tail, class OwnP = void>
+__device__ __forceinline__ void syn_interp_gm2(int wave, const SynLds &L, Stamps &st, Tail &&tail,
+                                               const Plane16 *own = nullptr) {
   using P = RestorePrograms<K, N, WV>;
   constexpr bool kPrio = SynShape<K, N, WV>::kPrio;
   constexpr int H = K / 2, kWpf = WV / 4, kWpq = WV / 2;
   if constexpr (W < WV) {
-    if (wave != W) return syn_interp_gm2<K, N, WV, W + 1>(wave, L, st, tail);
+    if (wave != W) return syn_interp_gm2<K, N, WV, W + 1, Tail &, OwnP>(wave, L, st, tail, own);
     uint32_t cells[16 * (K / WV)];
     uint32_t acc[64];
     auto cell = [&](int c) -> uint32_t(&)[16] { return *reinterpret_cast<uint32_t(*)[16]>(acc + 16 * c); };
     // S1: levels 1 and 2 on this wave's slots 4W..4W+3 (only this wave touches them)
     syn_prio<1, kPrio && (VDS_GM2_PRIO & 1)>();
-    P::gm_s1_(W, L, acc);
+    if constexpr (__is_same(OwnP, void))
+      P::gm_s1_(W, L, acc);
+    else
+      P::gm_s1_(W, S1In<OwnP::kPoint[W]>{L, *own}, acc);
 #pragma unroll
     for (int c = 0; c < 4; ++c) syn_put_point(L, 4 * W + c, cell(c));
     syn_prio<0, kPrio && (VDS_GM2_PRIO & 1)>();
@@ -516,6 +533,38 @@ __device__ __forceinline__ void syn_scatter_fill(int wave, const SynLds &L, cons
   }
 }
 
+// Own-group fill (FillP::kOwn, xorprog.hpp emit_fill_own; k = 16 survivor
+// sets with one erased point in each wave's interpolation group 4w..4w+3):
+// wave W computes its group's erased point from all survivors -- its own
+// four from the stage-1 registers (OwnIn), the rest from LDS -- and S1 reads
+// it from registers (S1In), so nothing is written, zeroed or XORed into LDS
+// for it and no barrier separates the fill from S1.
+template <class F, class = void>
+struct FillOwn {
+  static constexpr bool value = false;
+};
+template <class F>
+struct FillOwn<F, decltype(void(F::kOwn))> {
+  static constexpr bool value = F::kOwn;
+};
+template <class FillP, int W>
+struct OwnIn {
+  const SynLds &L;
+  const Plane16 (&P)[4];
+  __device__ __forceinline__ u32x4 operator()(int idx) const {
+    const int i = FillRegIn<FillP, W>::slot(idx >> 2), g = idx & 3;
+    if (i >= 0) return u32x4{P[i].p[4 * g], P[i].p[4 * g + 1], P[i].p[4 * g + 2], P[i].p[4 * g + 3]};
+    return L(idx);
+  }
+};
+template <int WV, class FillP, int W>
+__device__ __forceinline__ void syn_own_fill(int wave, const SynLds &L, const Plane16 (&Ps)[4], Plane16 &own) {
+  if constexpr (W < WV) {
+    if (wave != W) return syn_own_fill<WV, FillP, W + 1>(wave, L, Ps, own);
+    FillP::template own<W>(OwnIn<FillP, W>{L, Ps}, own.p);
+  }
+}
+
 // Batch mode: the last tile of an object may run past its bytes.  Loads
 // beyond `valid` bytes read zeros and stores beyond it write nothing (byte by
 // byte for the one 16-byte piece that straddles the end).
@@ -617,6 +666,8 @@ template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false, class F
 __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   constexpr bool FILL = FillP::kFill >= 0;
   constexpr bool kScatter = FILL && FillP::kScatter;
+  constexpr bool kOwn = FILL && FillOwn<FillP>::value;
+  static_assert(!kOwn || (K == 16 && !REGEN && !BATCH && !RT), "the own-group fill is a k = 16 restore form");
   constexpr bool kSmall = FillP::kSmall;
   constexpr bool kPerm = FillP::kPerm;
   constexpr bool kMulti = FillP::kMulti;
@@ -752,7 +803,8 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     const int my_erased = RT ? K + wave : perm_tile ? K : (wave < S::kM ? erased_of(wave) : 0);
     // RT: this wave's slots, kept for phase 2; the scatter fill: its survivors (VDS_FILL_REGS)
     constexpr bool kFillRegs = kScatter && VDS_FILL_REGS && K == 16;
-    constexpr bool kKeepPs = RT || kFillRegs;
+    constexpr bool kKeepPs = RT || kFillRegs || kOwn;
+    Plane16 own;  // (own-group fill: this wave's group's erased point)
     static_assert(!kKeepPs || S::kLoadPer == 4, "four survivors per wave");
     Plane16 Ps[kKeepPs ? S::kLoadPer : 1];
 
@@ -1187,6 +1239,10 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       else
         syn_scatter_fill<WV, FillP, false, 0>(wave, L, {});
       if (!kLateLoad) prefetch(tile + t_step);
+    } else if constexpr (kOwn) {
+      // ---- 2 (own). this wave's group's erased point, kept in registers for S1
+      syn_own_fill<WV, FillP, 0>(wave, L, Ps, own);
+      if (!kLateLoad) prefetch(tile + t_step);
     } else if constexpr (kPerm) {
       phase_perm(TypeTag<FillP>{});
     } else if constexpr (kSmall) {
@@ -1212,7 +1268,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       phase_syn();
     }  // (phase 2)
     st.mark(5);
-    __syncthreads();
+    if constexpr (!kOwn) __syncthreads();  // (own-group fill: S1 reads only what stage 1 published)
     st.mark(6);
     if constexpr (REGEN) {
       // ---- 3'. regenerate: the recovered point e_w IS replica e_w's cells
@@ -1288,7 +1344,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
       // vector spill of before).  The other kernels keep the join: with the
       // tail in the branches the plain k = 32 kernel spilled 1,844 (the late
       // loads beside the staging).
-      constexpr bool kTailInWave = RT || kFillRegs;
+      constexpr bool kTailInWave = RT || kFillRegs || kOwn;
       auto tail = [&](uint32_t (&cells)[16 * S::kCells]) {
       if (kLateLoad && !BATCH) prefetch(tile + t_step);
       // this wave's copy-out: 1024 kChunks bytes at wofs of the tile's output
@@ -1433,7 +1489,9 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
         st.mark(17);
       }
       };
-      if constexpr (VDS_GM2 != 0 && kTailInWave) {
+      if constexpr (VDS_GM2 != 0 && kOwn) {
+        syn_interp_gm2<K, N, WV, 0, decltype(tail) &, FillP>(wave, L, st, tail, &own);
+      } else if constexpr (VDS_GM2 != 0 && kTailInWave) {
         syn_interp_gm2<K, N, WV, 0>(wave, L, st, tail);
       } else if constexpr (VDS_GM2 != 0) {
         uint32_t cells[16 * S::kCells];

@@ -92,6 +92,18 @@ constexpr bool fill_prefetch() { return VDS_JIT_PREFETCH != 0; }
 #define VDS_JIT_SCATTER 1
 #endif
 constexpr bool fill_scatter() { return VDS_JIT_SCATTER != 0; }
+// The own-group fill (xorprog.hpp emit_fill_own) for k = 16 sets with one
+// erased point in each wave's interpolation group, e.g. the headline set
+// {0, 5, 10, 15}: measured slower than the scatter fill and off by default
+// (-DVDS_JIT_OWN=1 builds it).  Same box, ABBA, 512 x 64 MiB
+// (profiles/round6/ab_own_fill.log): repair 13.15 ms (scatter) against 13.47
+// (own, Paar blocks of 3), 13.34 (blocks of 2), 13.56 (no block prefetch);
+// blocks of 4 spill 21 VGPRs.  Its 48 ds_read_b128 per lane of the other
+// waves' survivors and ~25% more XORs cost more than the barrier and the 32
+// ds_xor_b64 atomics per lane they replace.
+#ifndef VDS_JIT_OWN
+#define VDS_JIT_OWN 0
+#endif
 
 // JIT policy: 0 = off, 1 = background compile from a set's second use
 // (default), 2 = compile on the calling thread at the first use.  Initially
@@ -161,6 +173,8 @@ std::string kernel_source(const Key &key) {
     for (int a = 0; a < N; ++a)
       if (!((key.survivors >> a) & 1u)) tg.push_back(a);
     xorgen::emit_fill_scatter(s, "JitFill", K, sp, &tg);
+  } else if (VDS_JIT_OWN && xorgen::fill_own_eligible(K, sp)) {
+    xorgen::emit_fill_own(s, "JitFill", K, sp, fill_block(), fill_prefetch());
   } else if (fill_scatter()) {
     xorgen::emit_fill_scatter(s, "JitFill", K, sp);
   } else {

@@ -457,4 +457,62 @@ inline size_t emit_fill_scatter(std::string &s, const char *name, int K, const s
   return total;
 }
 
+// "Own-group" fill of one survivor set (k = 16, four waves; restore only):
+// when each wave's interpolation group {4w..4w+3} holds exactly one erased
+// point, wave w computes that point from all K survivors -- its own four
+// (ranks 4w..4w+3) from its stage-1 registers, the rest from LDS -- and
+// hands it to its S1 in registers (restore_syn.hpp OwnIn / kOwn): no LDS
+// atomics, no zeroed slots, and no barrier between the fill and S1.  The
+// row programs of emit_fill_programs, one per wave.  Returns 0 (nothing
+// emitted) when the set does not have one erased point per group.
+inline bool fill_own_eligible(int K, const std::vector<int> &spoints) {
+  if (K != 16) return false;
+  for (int w = 0; w < K / 4; ++w) {
+    int e = 0;
+    for (int a = 4 * w; a < 4 * w + 4; ++a) e += std::find(spoints.begin(), spoints.end(), a) == spoints.end();
+    if (e != 1) return false;
+  }
+  return true;
+}
+inline size_t emit_fill_own(std::string &s, const char *name, int K, const std::vector<int> &spoints, int pb,
+                            bool prefetch = true) {
+  if (!fill_own_eligible(K, spoints)) return 0;
+  std::vector<int> EU;  // ascending: EU[w] is the erased point of group w
+  for (int a = 0; a < K; ++a)
+    if (std::find(spoints.begin(), spoints.end(), a) == spoints.end()) EU.push_back(a);
+  const int F = (int)EU.size();
+  std::vector<uint32_t> A((size_t)F * K);
+  for (int m = 0; m < F; ++m)
+    for (int j = 0; j < K; ++j) {
+      uint32_t num = 1, den = 1;
+      for (int t = 0; t < K; ++t)
+        if (t != j) {
+          num = vds_ec::gf16_mul(num, (uint32_t)(EU[m] ^ spoints[t]));
+          den = vds_ec::gf16_mul(den, (uint32_t)(spoints[j] ^ spoints[t]));
+        }
+      A[(size_t)m * K + j] = vds_ec::gf16_mul(num, vds_ec::gf16_inv(den));
+    }
+  InputMap im;
+  im.map = spoints;
+  appendf(s, "struct %s {\n  static constexpr int kFill = %d;\n  static constexpr bool kScatter = false, kOwn = true;\n",
+          name, F);
+  appendf(s, "  static constexpr bool kSmall = false, kPerm = false, kMulti = false;\n");
+  appendf(s, "  static constexpr uint8_t kPoint[%d] = {", F);
+  for (int e : EU) appendf(s, "%d, ", e);
+  appendf(s, "};\n  static constexpr uint8_t kSurv[%d] = {", K);
+  for (int j = 0; j < K; ++j) appendf(s, "%d, ", spoints[j]);
+  appendf(s, "};\n");
+  const auto rows = all_bitrows(A, F, K);
+  size_t total = 0;
+  for (int m = 0; m < F; ++m) {
+    char nm[32];
+    std::snprintf(nm, sizeof nm, "own%d", m);
+    total += emit_program(s, nm, rows, K, row_range(16 * m, 16), pb, im, prefetch);
+  }
+  appendf(s, "  template <int W, typename In>\n  __device__ __forceinline__ static void own(const In &IN4, uint32_t (&acc)[16]) {\n");
+  for (int m = 0; m < F; ++m) appendf(s, "    %sif constexpr (W == %d) own%d(IN4, acc);\n", m ? "else " : "", m, m);
+  appendf(s, "  }\n};\n");
+  return total;
+}
+
 }  // namespace xorgen

@@ -328,3 +328,63 @@ def test_regenerate_same_set_two_small_sizes(gpu, k):
     torch.cuda.synchronize()
     for (host, reps), t, o in zip(objs, targets, outs):
         assert np.array_equal(o.cpu().numpy()[:L], O.encode(k, t[0], host)), t
+
+
+@pytest.mark.parametrize("k", [16, 32])
+def test_batch_planner_many_parts(gpu, k):
+    """A call large enough for the planner's eight parallel parts (>= 8192
+    objects), whose survivor sets repeat across parts and cover every route:
+    survivors exactly 0..k-1 (SMALL / PERM), the first k found at a low loss
+    rate (SMALL, the N = k + k/4 syndrome kernel; sets shared by many
+    objects), at a high loss rate (RT / RT2; sets nearly all distinct), and
+    permuted orders.  Every restored object equals its input and every
+    regenerated replica (the first lost one) equals the encoded replica, both
+    compared on the device."""
+    import torch
+    from vds_amd import _lib, chunk
+    n = 64 if k == 32 else 40
+    count, size = 9000, 2 * k * 37 + 5  # (odd: a non-zero trailer; one half tile per object)
+    L = chunk.replica_size(k, size)
+    Ls = -(-L // 256) * 256
+    inp = torch.empty(count * size, dtype=torch.uint8, device="cuda")
+    chunk.fill_splitmix_device(inp, count * size, SEED + 4242 + k)
+    reps = torch.zeros((n, count * Ls), dtype=torch.uint8, device="cuda")
+    chunk.encode_device(k, list(range(n)), inp, size, size, count, [reps[i].data_ptr() for i in range(n)], Ls)
+    rng = np.random.default_rng(77 + k)
+    kind = rng.choice(4, count, p=[0.2, 0.4, 0.3, 0.1])
+    loss = np.where(kind == 2, 0.25, 0.03)
+    lost = rng.random((count, n)) < loss[:, None]
+    lost[kind == 0, :k] = False  # survivors exactly 0..k-1 (the first k found)
+    lost[kind == 0, k] = True    # (and replica k lost: the first target is k)
+    lost[:, :k + 4][(~lost).sum(axis=1) < k] = False  # (every object restorable)
+    nodes = np.stack([np.flatnonzero(~lost[o])[:k] for o in range(count)]).astype(np.uint16)
+    perm = kind == 3
+    nodes[perm] = np.stack([rng.permutation(r) for r in nodes[perm]])
+    base = np.asarray([reps[i].data_ptr() for i in range(n)], dtype=np.uint64)
+    cp = (base[nodes] + (np.arange(count, dtype=np.uint64) * Ls)[:, None]).astype(np.uint64)
+    sizes = np.full(count, L, dtype=np.uint64)
+    pads = np.full(count, size % (2 * k), dtype=np.uint16)
+    out = torch.zeros(count * size, dtype=torch.uint8, device="cuda")
+    outs = (np.uint64(out.data_ptr()) + np.arange(count, dtype=np.uint64) * size).astype(np.uint64)
+    lib = _lib.lib()
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.check(lib.vds_ec_restore16_batch_device(k, count, nodes.ctypes.data_as(_lib.u16p), cp.ctypes.data_as(_lib.vpp),
+                                                 sizes.ctypes.data_as(_lib.u64p), pads.ctypes.data_as(_lib.u16p),
+                                                 outs.ctypes.data_as(_lib.vpp), 0, s))
+    rg = np.flatnonzero(lost.any(axis=1))
+    tg = np.argmax(lost[rg], axis=1).astype(np.uint16)
+    rgo = torch.zeros(len(rg) * Ls, dtype=torch.uint8, device="cuda")
+    rgp = (np.uint64(rgo.data_ptr()) + np.arange(len(rg), dtype=np.uint64) * Ls).astype(np.uint64)
+    rn, rc = np.ascontiguousarray(nodes[rg]), np.ascontiguousarray(cp[rg])
+    rs = np.full(len(rg), L, dtype=np.uint64)
+    _lib.check(lib.vds_ec_regenerate16_batch_device(k, len(rg), rn.ctypes.data_as(_lib.u16p), rc.ctypes.data_as(_lib.vpp),
+                                                    rs.ctypes.data_as(_lib.u64p), 1, tg.ctypes.data_as(_lib.u16p),
+                                                    rgp.ctypes.data_as(_lib.vpp), s))
+    torch.cuda.synchronize()
+    bad = (out.view(count, size) != inp.view(count, size)).any(dim=1).nonzero().flatten().tolist()
+    assert not bad, f"{len(bad)} restored objects differ, first {bad[:5]}"
+    want = reps.view(n, count, Ls)[torch.from_numpy(tg.astype(np.int64)).cuda(), torch.from_numpy(rg).cuda(), :L]
+    badr = (rgo.view(-1, Ls)[:, :L] != want).any(dim=1).nonzero().flatten().tolist()
+    assert not badr, f"{len(badr)} regenerated replicas differ, first {badr[:5]}"
+    # the routes the call took (the test is meant to cover them all)
+    assert (nodes < k + k // 4).all(axis=1).sum() > count // 2 and (~(nodes < k + k // 4).all(axis=1)).sum() > 100

@@ -1,7 +1,8 @@
 # Round 6: same-box ABBA A/B of the batch planner (default build: concurrent
 # plan claims, per-part indices) against ab/oldplan (round 5's serial plan
-# and index passes) on the live legs, 2 rounds.
+# and index passes) on the live legs, 2 rounds.  Argument: the variant under ab/ (default oldplan).
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp
+OTHER=${1:-oldplan}
 one() {  # one LIB TAG
   if [ "$1" = default ]; then
     timeout -k 10 300 python tools/live_prof.py --loss 0.02 0.25 > gpurun_out/r6c_$2.log 2>&1 || { tail -5 gpurun_out/r6c_$2.log; exit 1; }
@@ -20,6 +21,6 @@ for loss in ("0.02", "0.25"):
 print(" | ".join(out))
 PY
 }
-for r in 1; do
-  one default ${r}a; one oldplan ${r}b; one oldplan ${r}c; one default ${r}d
+for r in 1 2; do
+  one default ${r}a; one $OTHER ${r}b; one $OTHER ${r}c; one default ${r}d
 done

@@ -313,11 +313,22 @@ struct SynBatchBuild {
     uint8_t ms;
     uint16_t target;
   };
+  // A part's cache of the keys it has looked up in this call, in front of the
+  // shared table: a set that repeats within the part (most do at low loss
+  // rates) is answered from the part's own cache lines.  Direct-mapped;
+  // entries of an earlier call are told apart by the call's epoch.
+  static constexpr uint32_t kLocal = 1024;
+  struct LocalEntry {
+    uint64_t key;
+    uint32_t val, epoch;
+  };
   struct alignas(64) PartPlans {  // (one cache line apart: the parts write them concurrently)
     std::vector<uint32_t> hused;  // table entries this part claimed (cleared one by one when the table is reused)
     std::vector<PlanReq> reqs, miss;
+    std::vector<LocalEntry> local;
     uint32_t next[4];  // claims in each class
   };
+  uint32_t epoch = 0;
   PartPlans pp[kMaxParts];
   uint32_t dense[4 * kMaxParts + 1];   // first slot plan of each (class, part) region
   uint32_t cls_end[4] = {0, 0, 0, 0};  // dense class ranges: [cls_end[c - 1], cls_end[c])
@@ -360,6 +371,11 @@ struct SynBatchBuild {
       q.hused.clear();
       q.reqs.clear();
       for (uint32_t &x : q.next) x = 0;
+      if (q.local.empty()) q.local.assign(kLocal, LocalEntry{0, 0, 0});
+    }
+    if (++epoch == 0) {  // (wrapped: forget every cached key)
+      for (PartPlans &q : pp) q.local.assign(kLocal, LocalEntry{0, 0, 0});
+      epoch = 1;
     }
     hshift = 64 - bits;
   }
@@ -372,8 +388,16 @@ struct SynBatchBuild {
     // (keyed by set AND ms: a regenerate's route also depends on its targets,
     // so one set may meet two SMALL sizes in a call; PERM also by target)
     const uint64_t hk = seen | ((uint64_t)ms << 56) | (ms == kMsPerm ? (uint64_t)target << 48 : 0);
+    const uint64_t hash = hk * 0x9E3779B97F4A7C15ull;
+    LocalEntry &le = pp[part].local[(hash >> 54) & (kLocal - 1)];
+    if (le.key == hk && le.epoch == epoch) return le.val;
+    const uint32_t v = plan_of_shared(part, seen, ms, target, hk, hash);
+    le = LocalEntry{hk, v, epoch};
+    return v;
+  }
+  uint32_t plan_of_shared(unsigned part, uint64_t seen, uint32_t ms, uint32_t target, uint64_t hk, uint64_t hash) {
     const size_t mask = ht.size() - 1;
-    size_t i = (size_t)((hk * 0x9E3779B97F4A7C15ull) >> hshift);
+    size_t i = (size_t)(hash >> hshift);
     for (;;) {
       uint64_t cur = __atomic_load_n(&ht[i].key, __ATOMIC_ACQUIRE);
       if (cur == 0) {

@@ -332,7 +332,7 @@ def test_regenerate_same_set_two_small_sizes(gpu, k):
 
 @pytest.mark.parametrize("k", [16, 32])
 def test_batch_planner_many_parts(gpu, k):
-    """A call large enough for the planner's eight parallel parts (>= 8192
+    """A call large enough for the planner's sixteen parallel parts (>= 16384
     objects), whose survivor sets repeat across parts and cover every route:
     survivors exactly 0..k-1 (SMALL / PERM), the first k found at a low loss
     rate (SMALL, the N = k + k/4 syndrome kernel; sets shared by many
@@ -343,7 +343,7 @@ def test_batch_planner_many_parts(gpu, k):
     import torch
     from vds_amd import _lib, chunk
     n = 64 if k == 32 else 40
-    count, size = 9000, 2 * k * 37 + 5  # (odd: a non-zero trailer; one half tile per object)
+    count, size = 17000, 2 * k * 37 + 5  # (odd: a non-zero trailer; one half tile per object)
     L = chunk.replica_size(k, size)
     Ls = -(-L // 256) * 256
     inp = torch.empty(count * size, dtype=torch.uint8, device="cuda")

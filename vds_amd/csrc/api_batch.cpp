@@ -124,6 +124,7 @@ bool syn_plan_solve(uint32_t k, uint32_t n, uint64_t seen, SynBatchPlan *out, ui
 // inline.
 class HostPool {
  public:
+  static constexpr unsigned kMaxWorkers = 15;
   static HostPool &get() {
     static HostPool *p = new HostPool();  // never freed: detached workers outlive every caller
     return *p;
@@ -159,8 +160,12 @@ class HostPool {
     std::condition_variable cv;
   };
   HostPool() {
-    const unsigned hw = std::thread::hardware_concurrency();
-    nworkers_ = hw > 1 ? std::min(hw - 1, 7u) : 0u;
+    // the CPUs this process may run on (a GPU box's share of the host is 16;
+    // hardware_concurrency counts the whole machine)
+    unsigned hw = std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) hw = std::min(hw ? hw : 1024u, (unsigned)CPU_COUNT(&set));
+    nworkers_ = hw > 1 ? std::min(hw - 1, kMaxWorkers) : 0u;
     for (unsigned i = 0; i < nworkers_; ++i) std::thread([this] { loop(); }).detach();
   }
   static void work(Job &j) {
@@ -197,7 +202,7 @@ class HostPool {
 // fn(part, o0, o1) over [0, count) in at most kMaxParts contiguous ranges of
 // at least kMinPer objects; a call with the same count always makes the same
 // ranges, so a later pass can continue from per-part totals of an earlier one.
-constexpr unsigned kMaxParts = 8;
+constexpr unsigned kMaxParts = 16;
 inline unsigned batch_parts(uint32_t count) {
   constexpr uint32_t kMinPer = 1024;
   return std::min<uint32_t>(kMaxParts, std::max<uint32_t>(1, count / kMinPer));

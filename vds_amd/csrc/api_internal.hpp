@@ -28,6 +28,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <sched.h>
 #include <shared_mutex>
 #include <thread>
 #include <unordered_map>

@@ -146,10 +146,12 @@ int vds_ec_regenerate16_device(uint16_t k, const uint16_t *nodes, const uint8_t 
  * chunk_sizes[o], paddings[o]) bytes to outs[o].  Regenerate writes replica
  * targets[o*nt + i] (chunk_sizes[o] bytes, trailer included) to
  * outs[o*nt + i].  Objects whose survivors lie within the syndrome kernel's
- * points (k in {16, 32}, ids < k + k/4) share ONE launch; the others take
- * one launch each.  Every object is validated before anything is enqueued
+ * points (k in {16, 32}, ids < k + k/4) share ONE launch, those with other
+ * ids below 256 (same k) one runtime-coefficient launch; the rest take one
+ * launch each.  Every object is validated before anything is enqueued
  * (pointers, lengths, distinct ids: VDS_EC_ESINGULAR otherwise); nothing
- * synchronises.  Regenerate bytes as vds_ec_regenerate16_device.             */
+ * synchronises.  count < 2^30 (VDS_EC_EINVAL otherwise).  Regenerate bytes as
+ * vds_ec_regenerate16_device.                                                 */
 int vds_ec_restore16_batch_device(uint16_t k, uint32_t count, const uint16_t *nodes, const uint8_t *const *chunks,
                                   const uint64_t *chunk_sizes, const uint16_t *paddings, uint8_t *const *outs,
                                   unsigned flags, void *stream);

@@ -304,7 +304,10 @@ inline bool id_set(uint32_t k, const uint16_t *nd, uint64_t *seen, uint32_t *max
 inline uint32_t plan_class_rank(uint32_t ms) { return ms == 1 ? 0 : ms == 2 ? 1 : ms == kMsPerm ? 2 : 3; }
 struct SynBatchBuild {
   static constexpr uint32_t kPending = 0xFFFFFFFFu;
-  static constexpr int kRegionShift = 27;  // claim = (class * kMaxParts + part) << 27 | index within the region
+  // claim = (class * kMaxParts + part) << kRegionShift | index within the
+  // region (< the part's objects: < 2^26 for any count below 2^30)
+  static constexpr int kRegionShift = 26;
+  static_assert(4 * kMaxParts <= (1u << (32 - kRegionShift)), "claim regions fit in the claim's top bits");
   uint32_t k, n;
   bool regen = false;
   ParamSlot *slot = nullptr;
@@ -876,6 +879,7 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
                          hipStream_t s) {
   if (k == 0 || (count && (!nodes || !chunks || !chunk_sizes || !paddings || !outs))) return VDS_EC_EINVAL;
   if (count == 0) return VDS_EC_OK;
+  if (count >= (1u << 30)) return VDS_EC_EINVAL;  // (the planner's claim numbers; a slot that size could not be pinned anyway)
   const uint32_t n = k + k / 4;
   const bool batch_ok = !(flags & VDS_EC_F_CELLS) && k % 4 == 0 && has_restore_syn(k, n);
   const bool syn = batch_ok && !restore_path_override_bs();
@@ -998,6 +1002,7 @@ int regenerate_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, c
                             hipStream_t s) {
   if (k == 0 || (count && (!nodes || !chunks || !chunk_sizes || (nt && (!targets || !outs))))) return VDS_EC_EINVAL;
   if (count == 0 || nt == 0) return VDS_EC_OK;
+  if (count >= (1u << 30)) return VDS_EC_EINVAL;  // (as restore_batch_device)
   // Routes as restore_batch_device's; the syndrome kernel only when every
   // target is one of the object's erased points (each at most once: wave w
   // recovers the w-th erased point, ascending); an RT object carries at most

@@ -257,6 +257,16 @@ constexpr uint8_t kMsPerm = 3;
 #define VDS_BATCH_SMALL 1
 #endif
 constexpr bool small_enabled() { return VDS_BATCH_SMALL != 0; }
+// Restore objects of the N = k + k/4 syndrome class at k = 32 (survivors
+// within 0..39 beyond the SMALL sizes) through the RT batch instead
+// (study switch, -DVDS_BATCH_N_TO_RT=1): at p = 0.25 those objects' erased
+// sets are nearly all distinct, so their syndrome tiles run half empty, while
+// RT tiles pair any two objects.  Same box, ABBA (profiles/round6/planner/
+// ab_n40_to_rt.log): device time per live call 2.08-2.09 -> 2.03-2.05 ms at
+// p = 0.25, unchanged at p = 0.02 -- within the rates' noise; off.
+#ifndef VDS_BATCH_N_TO_RT
+#define VDS_BATCH_N_TO_RT 0
+#endif
 // The smallest SMALL ms whose points 0..k+ms-1 hold every survivor (maxid), or 0.
 uint8_t small_ms_for(uint32_t k, uint32_t maxid) {
   if (!small_enabled()) return 0;
@@ -920,7 +930,7 @@ int restore_batch_device(uint32_t k, uint32_t count, const uint16_t *nodes, cons
       const bool fits = need <= 0xFFFFFFFFull - kHalfStripes;
       if (need == 0) {
         f.route = kRouteSkip;
-      } else if (syn && fits && maxid < n) {
+      } else if (syn && fits && maxid < n && !(VDS_BATCH_N_TO_RT && k == 32 && small_ms_for(k, maxid) == 0)) {
         f.route = kRouteSyn;
         f.ms = small_ms_for(k, maxid);
         f.plan = bb.plan_of(part, f.seen, f.ms, 0);

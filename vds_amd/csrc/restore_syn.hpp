@@ -53,6 +53,12 @@ struct SynShape {
 #ifndef VDS_DIAG_STAMPS
 #define VDS_DIAG_STAMPS 0
 #endif
+// Load study (wrong results, timing only; with the stamps): 1 = every tile
+// after the first reloads the first tile's survivors (L2 hits), 2 = no loads
+// after the first tile (zero survivors).  Round 6, k = 32 (§3.7 of DESIGN.md).
+#ifndef VDS_DIAG_LOADS
+#define VDS_DIAG_LOADS 0
+#endif
 
 // Wave priority by phase when two workgroups share a CU (k = 16).  Their
 // phases drift apart; the workgroup in stage 1 (survivors -> LDS planes) and
@@ -748,9 +754,9 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   Stamps st;
   st.init();
   auto prefetch = [&](uint32_t t) {
-    if (t < tr.end) {
+    if (t < tr.end && (VDS_DIAG_LOADS != 2 || t == tr.first)) {
       st.rt((t - tr.first) / tr.step);
-      load(t);
+      load(VDS_DIAG_LOADS == 1 ? tr.first : t);
     } else {
 #pragma unroll
       for (int s = 0; s < S::kLoadPer; ++s)

@@ -166,6 +166,9 @@ std::string kernel_source(const Key &key) {
 #if VDS_DIAG_STAMPS
   xorgen::appendf(s, "#define VDS_DIAG_STAMPS 1\n");  // (phase stamps: vds_ec_diag_jit_stamps)
 #endif
+#if defined(VDS_DIAG_LOADS) && VDS_DIAG_LOADS
+  xorgen::appendf(s, "#define VDS_DIAG_LOADS %d\n", VDS_DIAG_LOADS);  // (load study, restore_syn.hpp)
+#endif
   xorgen::appendf(s, "#define VDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)\n#include \"restore_syn.hpp\"\n");
   xorgen::appendf(s, "namespace vds_ec {\n#include \"generated/restore_%d_%d_w%d.inc\"\n", K, N, WV);
   if (key.regen) {  // every erased point, in ascending order (= SynRestoreArgs::erased)

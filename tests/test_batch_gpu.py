@@ -388,3 +388,49 @@ def test_batch_planner_many_parts(gpu, k):
     assert not badr, f"{len(badr)} regenerated replicas differ, first {badr[:5]}"
     # the routes the call took (the test is meant to cover them all)
     assert (nodes < k + k // 4).all(axis=1).sum() > count // 2 and (~(nodes < k + k // 4).all(axis=1)).sum() > 100
+
+
+def test_restore_batch_dual_tiles(gpu):
+    """k = 32, n = 40: objects whose erased sets are all different (the live
+    shape at a high loss rate) -- each plan's odd half goes into a dual tile
+    with another plan's (kTileDual: two survivor layouts and two coefficient
+    walks in one tile).  Codeword and non-codeword survivors, objects of one
+    to three halves and ragged sizes, a few sets shared; every object against
+    the oracle's restore of the same chunks."""
+    import torch
+    from vds_amd import chunk
+    k, n = 32, 40
+    rng = np.random.default_rng(4242)
+    half = 1024 * 2 * k
+    sizes = ([half] * 23 + [half - 2 * k * 3 - 1, 2 * half, 3 * half + 5, 1, 2 * k * 11 + 7] +
+             [int(x) for x in rng.integers(1, 3 * half, 10)])
+    objs = _objects(torch, k, n, sizes, seed=1300)
+    sets = []
+    while len(sets) < len(sizes):
+        er = set(rng.choice(n, n - k, replace=False).tolist())
+        nd = [r for r in range(n) if r not in er]
+        if max(nd) >= k + 2 and min(er) < k:  # the N-point syndrome class (not SMALL)
+            sets.append(nd)
+    sets[5] = sets[4]  # two objects of one plan beside the singles
+    nodes, chunks, csz, pads, outs, data = [], [], [], [], [], []
+    for i, ((host, reps), size) in enumerate(zip(objs, sizes)):
+        nd = sets[i] if i % 3 else list(rng.permutation(sets[i]))
+        if i % 2:  # non-codeword survivors: random cells in every chunk (trailers kept)
+            for r in nd:
+                reps[r][:-2].copy_(torch.from_numpy(rng.integers(0, 256, reps[r].numel() - 2, dtype=np.uint8)).cuda())
+        nodes.append(nd)
+        chunks.append([reps[r].data_ptr() for r in nd])
+        csz.append(reps[0].numel())
+        pads.append(size % (2 * k))
+        outs.append(torch.full((size + 4 * k,), 0xA5, dtype=torch.uint8, device="cuda"))
+        data.append([reps[r].cpu().numpy() for r in nd])
+    chunk.restore_batch_device(k, nodes, chunks, csz, pads, [o.data_ptr() for o in outs])
+    torch.cuda.synchronize()
+    for i, ((host, reps), size, out, nd) in enumerate(zip(objs, sizes, outs, nodes)):
+        got = out.cpu().numpy()
+        ref = O.restore(k, nd, data[i])
+        assert ref is not None and ref.size == size
+        assert np.array_equal(got[:size], ref), (i, size, nd)
+        if i % 2 == 0:
+            assert np.array_equal(got[:size], host), (i, size)
+        assert (got[size:] == 0xA5).all(), (i, size)

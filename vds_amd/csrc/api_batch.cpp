@@ -296,6 +296,13 @@ inline bool id_set(uint32_t k, const uint16_t *nd, uint64_t *seen, uint32_t *max
   return !wide || ids_distinct(k, nd);
 }
 
+// Dual syndrome tiles (restore_syn.hpp VDS_BATCH_DUAL; the host pairs only
+// what the kernels were built with)
+#ifndef VDS_BATCH_DUAL
+#define VDS_BATCH_DUAL 1
+#endif
+constexpr bool dual_enabled() { return VDS_BATCH_DUAL != 0; }
+
 // Host-side builder of one k_restore_syn batch launch, written straight into
 // a pinned parameter slot: objs (and the empty object), then tiles, then
 // plans.  plan_of() resolves survivor sets to plans and fill() writes
@@ -538,26 +545,38 @@ struct SynBatchBuild {
   // Pair the halves of each plan into tiles, stage and launch (regenerate:
   // the last half of every object also copies its trailer cell, and the tail
   // kernel then writes the reference route's last cell and trailer).
+  // Restore at k = 32: the odd half of each N-point syndrome plan (class 3)
+  // goes into a dual tile with another plan's (kTileDual, after class 3's
+  // own tiles) instead of a tile of its own beside the empty object.
   int launch(bool regen, hipStream_t s) {
     if (nobj == 0) return hip_status(param_release(slot, s));
     const uint32_t empty = nobj;
     std::memset(&objs[empty], 0, sizeof(SynBatchObj));
     const uint32_t np = cls_end[3];
     const uint32_t base[5] = {0, cls_end[0], cls_end[1], cls_end[2], cls_end[3]};
+    const bool dual = dual_enabled() && !regen && k == 32;
     std::vector<uint64_t> &first = first_, &used = used_;
     first.assign(np + 1, 0);  // tile offset of each plan
     used.assign(np, 0);
     for (uint32_t o = 0; o < nobj; ++o) first[obj_plan[o] + 1] += obj_halves[o];
-    for (size_t p = 0; p < np; ++p) first[p + 1] = first[p] + (first[p + 1] + 1) / 2;
-    const uint64_t ntiles = first[np];
+    uint64_t singles = 0;  // dual: class 3's odd halves
+    for (size_t p = 0; p < np; ++p) {
+      const uint64_t h = first[p + 1];
+      const bool pair_out = dual && p >= base[3] && (h & 1u);
+      singles += pair_out;
+      first[p + 1] = first[p] + (pair_out ? h / 2 : (h + 1) / 2);
+    }
+    const uint64_t ndual = (singles + 1) / 2;
+    const uint64_t ntiles = first[np] + ndual;
     if (ntiles > cap_tiles || ntiles > 0xFFFFFFFFull) {
       (void)param_release(slot, s);
       return VDS_EC_EINVAL;
     }
-    // classes (contiguous plan and tile ranges)
+    // classes (contiguous plan and tile ranges; the dual tiles end class 3's)
     const uint32_t *bound = base + 1;
+    auto cls_tiles = [&](int c) { return first[base[c + 1]] - first[base[c]] + (c == 3 ? ndual : 0); };
     int ncls = 0;
-    for (int c = 0; c < 4; ++c) ncls += first[base[c + 1]] > first[base[c]];
+    for (int c = 0; c < 4; ++c) ncls += cls_tiles(c) > 0;
     // MULTI (ncls > 1): tile t goes to position pos(t), so that each XCD's
     // contiguous eighth of the launch (tile_range) gets every eighth tile --
     // the same mix of classes, whose tiles cost differently
@@ -571,10 +590,20 @@ struct SynBatchBuild {
     for (size_t p = 0; p < np; ++p)
       for (uint64_t t = first[p]; t < first[p + 1]; ++t)
         tiles[pos(t)] = SynBatchTile{{empty, empty}, {0, 0}, (uint32_t)p, 0, 0, 0};
+    uint64_t si = 0;  // dual: singles placed
     for (uint32_t o = 0; o < nobj; ++o) {
       const uint32_t p = obj_plan[o];
       for (uint32_t h = 0; h < obj_halves[o]; ++h) {
         const uint64_t i = used[p]++;
+        if (dual && p >= base[3] && i == 2 * (first[p + 1] - first[p])) {  // the plan's odd half
+          SynBatchTile &t = tiles[pos(first[np] + si / 2)];
+          if ((si & 1) == 0)
+            t = SynBatchTile{{o, empty}, {h * kHalfStripes, 0}, p, 0, 0, 0};
+          else
+            t.obj[1] = o, t.stripe0[1] = h * kHalfStripes, t.mode = kTileDual;
+          ++si;
+          continue;
+        }
         SynBatchTile &t = tiles[pos(first[p] + i / 2)];
         t.obj[i & 1] = o;
         t.stripe0[i & 1] = h * kHalfStripes;
@@ -597,7 +626,7 @@ struct SynBatchBuild {
       }
       uint32_t p0 = 0;
       for (int c = 0; c < 4 && e == hipSuccess && ncls == 1; ++c) {
-        const uint64_t t0 = first[p0], t1 = first[bound[c]];
+        const uint64_t t0 = first[p0], t1 = first[bound[c]] + (c == 3 ? ndual : 0);
         p0 = bound[c];
         if (t1 == t0) continue;
         sa.tiles = dt + t0;

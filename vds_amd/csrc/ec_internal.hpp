@@ -218,8 +218,11 @@ struct SynBatchTile {
   uint32_t plan;        // (RT: unused)
   uint32_t trailer;     // regenerate: bit h = half h also copies its object's trailer cell
   uint32_t nm;          // RT: rows of the tile = max ne over its halves
-  uint32_t mode;        // RT: SynBatchRt::mode of both halves (the host never pairs two modes)
+  uint32_t mode;        // RT: SynBatchRt::mode of both halves (the host never pairs two modes); else kTileDual or 0
 };
+// mode of a syndrome-route restore tile whose halves are objects of different
+// plans (plan = half 0's; half 1's from its object: restore_syn.hpp kDual)
+constexpr uint32_t kTileDual = 2;
 
 // Reference-route tail of a regenerate.  The reference repairs a replica by
 // restoring the object -- trimmed to E bytes (chunk.h:415-419, 437-438) --

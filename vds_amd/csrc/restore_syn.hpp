@@ -463,6 +463,25 @@ __device__ __forceinline__ void rec_dual_x(Plane16 &acc, const Plane16 &t, const
         [pa] "i"(pa), [pb] "i"(pb)
       : "scc");
 }
+// The same with the two masks given: acc ^= (T & ma) ^ (T1 & mb), ma / mb in
+// {0, kRtH0, kRtH1, ~0} (a dual syndrome tile's bit pair of one row: each
+// half's own coefficient bit).
+__device__ __forceinline__ void rec_dual_m(Plane16 &acc, const Plane16 &t, const Plane16 &t1, uint32_t ma,
+                                           uint32_t mb) {
+  uint32_t tm;
+  asm volatile(
+      "s_cmp_eq_u32 %[ma], 0\n"
+      "s_cbranch_scc1 1f\n"
+      "v_mov_b32 %[tm], %[ma]\n" VDS_RS_SEQ(VDS_RD_MA)
+      "1:\n"
+      "s_cmp_eq_u32 %[mb], 0\n"
+      "s_cbranch_scc1 2f\n"
+      "v_mov_b32 %[tm], %[mb]\n" VDS_RS_SEQ(VDS_RD_MB)
+      "2:\n"
+      : VDS_RS_LIST(VDS_RS_C), [tm] "=&v"(tm)
+      : VDS_RS_LIST(VDS_RS_A), VDS_RS_LIST(VDS_RS_B), [ma] "s"(ma), [mb] "s"(mb)
+      : "scc");
+}
 #undef VDS_RD_MA
 #undef VDS_RD_MB
 #undef VDS_RS_C
@@ -668,6 +687,16 @@ template <int K, int MS> struct SmallSyn;
 #ifndef VDS_SYN_RT2
 #define VDS_SYN_RT2 1  // (A/B: 0 compiles the RT kernels without the RT2 rows)
 #endif
+// Dual syndrome tiles (batch restore, k = 32; SynBatchTile::mode kTileDual):
+// the two halves are objects of different plans -- the N-point class's single
+// halves, which at a high loss rate are nearly every object (distinct erased
+// sets).  The syndrome programs serve both halves as they are; stage 1 places
+// each half's survivors at its own points and phase 2 walks each half's
+// coefficients under its half mask.  (A/B: 0 compiles the batch kernels
+// without it; the host pairs only what the kernels support, api_batch.cpp.)
+#ifndef VDS_BATCH_DUAL
+#define VDS_BATCH_DUAL 1
+#endif
 template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false, class FillP = NoFill>
 __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
   constexpr bool FILL = FillP::kFill >= 0;
@@ -818,11 +847,26 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     // PERM evaluations of P0 and |E| x |E| runtime products
     constexpr bool kRt2 = VDS_SYN_RT2 && RT && !REGEN && K == 32 && N >= K + 8;
     const bool rt2_tile = kRt2 && s_ld(&a.tiles[tile].mode) == 1u;
+    // dual syndrome tile: half 1's plan (half 0's is the tile's)
+    constexpr bool kDual = VDS_BATCH_DUAL && BATCH && !RT && !REGEN && !FILL && !kSmall && !kPerm && K == 32;
+    const bool dual_tile = kDual && s_ld(&a.tiles[tile].mode) == kTileDual;
+    const SynBatchPlan *pl1 = kDual && dual_tile ? &a.plans[s_ld(&half_obj(tile, 1).plan)] : pl;
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
     syn_prio<1, kPrio>();
     uint64_t bor[2] = {0, 0};  // RT restore: borrowed slots of each half
     {
-      if (wave < S::kM && (!RT || REGEN) && !FILL && (!perm_tile || wave == 0)) {
+      if constexpr (kDual) {
+        if (dual_tile) {  // every slot zero first: a slot may take its halves from two waves
+          static_assert(N % WV == 0, "dual tiles: whole slots per wave");
+          const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int i = 0; i < N / WV; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) L.put(4 * ((N / WV) * wave + i) + g, z);
+          __syncthreads();
+        }
+      }
+      if (wave < S::kM && (!RT || REGEN) && !FILL && (!perm_tile || wave == 0) && !(kDual && dual_tile)) {
         const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int g = 0; g < 4; ++g) L.put(4 * my_erased + g, z);
@@ -876,7 +920,19 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
           if constexpr (kKeepPs)
 #pragma unroll
             for (int b = 0; b < 16; ++b) Ps[s].p[b] = Pl[b];
-          syn_put_point(L, (int)s_ld_u8(BATCH ? pl->point : a.point, wave * S::kLoadPer + s), Pl);
+          const int p0 = (int)s_ld_u8(BATCH ? pl->point : a.point, wave * S::kLoadPer + s);
+          const int p1 = kDual && dual_tile ? (int)s_ld_u8(pl1->point, wave * S::kLoadPer + s) : p0;
+          if (p0 == p1) {
+            syn_put_point(L, p0, Pl);
+          } else {  // (dual: each half's bits at its own point)
+            Plane16 v;
+#pragma unroll
+            for (int b = 0; b < 16; ++b) v.p[b] = Pl[b] & kRtH0;
+            lds_xor_point(L, p0, v);
+#pragma unroll
+            for (int b = 0; b < 16; ++b) v.p[b] = Pl[b] & kRtH1;
+            lds_xor_point(L, p1, v);
+          }
         }
       }
     }
@@ -970,6 +1026,52 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
         // accumulators would not fit beside the prefetched survivors)
         constexpr int kMC = S::kM <= 4 ? S::kM : 4;
         if constexpr (kMC < S::kM) __syncthreads();  // every wave is done reading the zeroed erased planes
+        if constexpr (kDual) {
+          if (dual_tile) {
+            // each half's bit pair of row m as a mask pair (rolled over the
+            // pairs: the masks are run-time values, one body serves them all)
+#pragma unroll
+            for (int m0 = 0; m0 < S::kM; m0 += kMC) {
+              Plane16 ce[kMC];
+#pragma unroll
+              for (int m = 0; m < kMC; ++m) ce[m] = plane_zero();
+              Plane16 tt = t;
+#pragma clang loop unroll(disable)
+              for (int b = 0; b < 16; b += 2) {
+                const Plane16 t1 = plane_mulx(tt);
+#pragma unroll
+                for (int m = 0; m < kMC; ++m) {
+                  const uint32_t sh = 8u * (uint32_t)(b & 3) + (uint32_t)wave;
+                  const uint32_t two0 = (s_ld(&pl->solve_sel[m0 + m][b >> 2]) >> sh) & 0x101u;
+                  const uint32_t two1 = (s_ld(&pl1->solve_sel[m0 + m][b >> 2]) >> sh) & 0x101u;
+                  const uint32_t ma = (two0 & 1u ? kRtH0 : 0u) | (two1 & 1u ? kRtH1 : 0u);
+                  const uint32_t mb = (two0 & 0x100u ? kRtH0 : 0u) | (two1 & 0x100u ? kRtH1 : 0u);
+                  rec_dual_m(ce[m], tt, t1, ma, mb);
+                }
+                tt = plane_mulx(t1);
+              }
+              st.mark(3);
+              if constexpr (kMC == S::kM) __syncthreads();
+              st.mark(4);
+#pragma unroll
+              for (int m = 0; m < kMC; ++m) {
+                const int e0 = (int)s_ld_u8(pl->erased, m0 + m), e1 = (int)s_ld_u8(pl1->erased, m0 + m);
+                if (e0 == e1) {
+                  lds_xor_point(L, e0, ce[m]);
+                } else {
+                  Plane16 v;
+#pragma unroll
+                  for (int q = 0; q < 16; ++q) v.p[q] = ce[m].p[q] & kRtH0;
+                  lds_xor_point(L, e0, v);
+#pragma unroll
+                  for (int q = 0; q < 16; ++q) v.p[q] = ce[m].p[q] & kRtH1;
+                  lds_xor_point(L, e1, v);
+                }
+              }
+            }
+            return;
+          }
+        }
 #pragma unroll
         for (int m0 = 0; m0 < S::kM; m0 += kMC) {
           Plane16 ce[kMC];

@@ -392,7 +392,7 @@ def test_batch_planner_many_parts(gpu, k):
 
 def test_restore_batch_dual_tiles(gpu):
     """k = 32, n = 40: objects whose erased sets are all different (the live
-    shape at a high loss rate) -- each plan's odd half goes into a dual tile
+    shape at a high loss rate) -- restore and regenerate: each plan's odd half goes into a dual tile
     with another plan's (kTileDual: two survivor layouts and two coefficient
     walks in one tile).  Codeword and non-codeword survivors, objects of one
     to three halves and ragged sizes, a few sets shared; every object against
@@ -425,6 +425,11 @@ def test_restore_batch_dual_tiles(gpu):
         outs.append(torch.full((size + 4 * k,), 0xA5, dtype=torch.uint8, device="cuda"))
         data.append([reps[r].cpu().numpy() for r in nd])
     chunk.restore_batch_device(k, nodes, chunks, csz, pads, [o.data_ptr() for o in outs])
+    # regenerate: two erased points below n of each object (the repair
+    # route's result: restore, then re-encode the E bytes)
+    targets = [sorted(rng.choice([r for r in range(n) if r not in nd], 2, replace=False).tolist()) for nd in nodes]
+    rg = [[torch.full((c + 8,), 0x5A, dtype=torch.uint8, device="cuda") for _ in tg] for c, tg in zip(csz, targets)]
+    chunk.regenerate_batch_device(k, nodes, chunks, csz, targets, [[x.data_ptr() for x in r] for r in rg])
     torch.cuda.synchronize()
     for i, ((host, reps), size, out, nd) in enumerate(zip(objs, sizes, outs, nodes)):
         got = out.cpu().numpy()
@@ -434,3 +439,7 @@ def test_restore_batch_dual_tiles(gpu):
         if i % 2 == 0:
             assert np.array_equal(got[:size], host), (i, size)
         assert (got[size:] == 0xA5).all(), (i, size)
+        for t, x in zip(targets[i], rg[i]):
+            g = x.cpu().numpy()
+            assert np.array_equal(g[:csz[i]], O.encode(k, t, ref)), (i, t)
+            assert (g[csz[i]:] == 0x5A).all()

@@ -545,7 +545,7 @@ struct SynBatchBuild {
   // Pair the halves of each plan into tiles, stage and launch (regenerate:
   // the last half of every object also copies its trailer cell, and the tail
   // kernel then writes the reference route's last cell and trailer).
-  // Restore at k = 32: the odd half of each N-point syndrome plan (class 3)
+  // At k = 32 the odd half of each N-point syndrome plan (class 3)
   // goes into a dual tile with another plan's (kTileDual, after class 3's
   // own tiles) instead of a tile of its own beside the empty object.
   int launch(bool regen, hipStream_t s) {
@@ -554,7 +554,7 @@ struct SynBatchBuild {
     std::memset(&objs[empty], 0, sizeof(SynBatchObj));
     const uint32_t np = cls_end[3];
     const uint32_t base[5] = {0, cls_end[0], cls_end[1], cls_end[2], cls_end[3]};
-    const bool dual = dual_enabled() && !regen && k == 32;
+    const bool dual = dual_enabled() && k == 32;
     std::vector<uint64_t> &first = first_, &used = used_;
     first.assign(np + 1, 0);  // tile offset of each plan
     used.assign(np, 0);
@@ -601,6 +601,7 @@ struct SynBatchBuild {
             t = SynBatchTile{{o, empty}, {h * kHalfStripes, 0}, p, 0, 0, 0};
           else
             t.obj[1] = o, t.stripe0[1] = h * kHalfStripes, t.mode = kTileDual;
+          if (regen && h + 1 == obj_halves[o]) t.trailer |= 1u << (si & 1);
           ++si;
           continue;
         }

@@ -220,7 +220,7 @@ struct SynBatchTile {
   uint32_t nm;          // RT: rows of the tile = max ne over its halves
   uint32_t mode;        // RT: SynBatchRt::mode of both halves (the host never pairs two modes); else kTileDual or 0
 };
-// mode of a syndrome-route restore tile whose halves are objects of different
+// mode of a syndrome-route tile whose halves are objects of different
 // plans (plan = half 0's; half 1's from its object: restore_syn.hpp kDual)
 constexpr uint32_t kTileDual = 2;
 

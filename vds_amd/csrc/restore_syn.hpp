@@ -687,15 +687,22 @@ template <int K, int MS> struct SmallSyn;
 #ifndef VDS_SYN_RT2
 #define VDS_SYN_RT2 1  // (A/B: 0 compiles the RT kernels without the RT2 rows)
 #endif
-// Dual syndrome tiles (batch restore, k = 32; SynBatchTile::mode kTileDual):
+// Dual syndrome tiles (batched restore and regenerate, k = 32;
+// SynBatchTile::mode kTileDual):
 // the two halves are objects of different plans -- the N-point class's single
 // halves, which at a high loss rate are nearly every object (distinct erased
 // sets).  The syndrome programs serve both halves as they are; stage 1 places
 // each half's survivors at its own points and phase 2 walks each half's
-// coefficients under its half mask.  (A/B: 0 compiles the batch kernels
+// coefficients under its half mask (regenerate: and stores each half's own
+// erased points).  (A/B: 0 compiles the batch kernels
 // without it; the host pairs only what the kernels support, api_batch.cpp.)
 #ifndef VDS_BATCH_DUAL
 #define VDS_BATCH_DUAL 1
+#endif
+// RT2 (c): the extra rows' columns spread over all eight waves (A/B: 0 = rows
+// w and w + 8 whole on wave w).
+#ifndef VDS_RT2_SPREAD
+#define VDS_RT2_SPREAD 1
 #endif
 template <int K, int N, int WV, bool REGEN, bool BATCH, bool RT = false, class FillP = NoFill>
 __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
@@ -848,7 +855,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
     constexpr bool kRt2 = VDS_SYN_RT2 && RT && !REGEN && K == 32 && N >= K + 8;
     const bool rt2_tile = kRt2 && s_ld(&a.tiles[tile].mode) == 1u;
     // dual syndrome tile: half 1's plan (half 0's is the tile's)
-    constexpr bool kDual = VDS_BATCH_DUAL && BATCH && !RT && !REGEN && !FILL && !kSmall && !kPerm && K == 32;
+    constexpr bool kDual = VDS_BATCH_DUAL && BATCH && !RT && !FILL && !kSmall && !kPerm && K == 32;
     const bool dual_tile = kDual && s_ld(&a.tiles[tile].mode) == kTileDual;
     const SynBatchPlan *pl1 = kDual && dual_tile ? &a.plans[s_ld(&half_obj(tile, 1).plan)] : pl;
     // ---- 1. survivors -> planes of their points; waves < M zero one erased point
@@ -1123,15 +1130,29 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
           // registers, a second one reloaded from the survivors' bytes, so
           // the registers do not live across the first group), (b) the PERM
           // program's P0(b_j) of both halves (reads through c -> c ^ t'_h,
-          // merged by half) into the same slots, barrier, (c) rows m = wave,
-          // wave + 8 accumulate sum_j c[m][j] r_j (two rows per walk of each
-          // r_j's x^b chain); after the last group (d) P(e_m) into the erased
+          // merged by half) into the same slots, barrier, (c) the wave's rows
+          // accumulate sum_j c[m][j] r_j (two rows per walk of each r_j's x^b
+          // chain; see row[] below); after the last group (d) P(e_m) into the erased
           // slots (zero in their halves until then: the P0 reads need that)
           const uint8_t *ep0 = d0.rt.epoint, *ep1 = d1.rt.epoint, *sp0 = d0.rt.spoint, *sp1 = d1.rt.spoint;
           Plane16 racc[2];
           racc[0] = plane_zero();
           racc[1] = plane_zero();
-          const bool two_rows = (uint32_t)wave + 8u < rt_rows;
+          // (c)'s rows of this wave: row w over every column and, with E =
+          // rows - 8 > 0, extra row 8 + e (e = w E / 8) over the columns j with
+          // j mod parts = part -- the extra rows' columns spread over all eight
+          // waves, whose partial sums (d) adds into the erased slots.  (Rows w
+          // and w + 8 over every column put two rows on waves 0..E-1 and one on
+          // the rest: those waves set the barrier's pace, RT stamps r6o.)
+          const uint32_t xE = rt_rows > 8u ? rt_rows - 8u : 0u;
+          uint32_t xpart = 0, xparts = 1;
+          const uint32_t row[2] = {(uint32_t)wave, VDS_RT2_SPREAD ? 8u + (uint32_t)wave * xE / 8u : (uint32_t)wave + 8u};
+          const bool has_row[2] = {(uint32_t)wave < rt_rows, VDS_RT2_SPREAD ? xE != 0u : (uint32_t)wave + 8u < rt_rows};
+          if (VDS_RT2_SPREAD && xE != 0u) {
+            const uint32_t e = row[1] - 8u, w0 = (8u * e + xE - 1u) / xE, w1 = (8u * (e + 1u) + xE - 1u) / xE;
+            xpart = (uint32_t)wave - w0;
+            xparts = w1 - w0;
+          }
           // (a), first group: from the stage-1 registers (dead after this)
 #pragma unroll
           for (int sl = 0; sl < S::kLoadPer; ++sl) {
@@ -1187,6 +1208,7 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
                   }
               }
             }
+            st.mark(2);  // (RT2 stamps: 2 = (a), 3 = (b), 4 = its barrier, 19 = (c), 5 = (d))
             // (b)
 #pragma clang loop unroll(disable)
             for (uint32_t j = g0; j < g1; ++j) {
@@ -1212,15 +1234,18 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
               PermSyn<K>::part(wave, in, pacc);
               lds_xor_point(L, K + (int)(j - g0), *reinterpret_cast<const Plane16 *>(pacc));
             }
+            st.mark(3);
             __syncthreads();  // the group's r_j are whole
+            st.mark(4);
             // (c)
-            if ((uint32_t)wave < rt_rows) {
+            if (has_row[0]) {
 #pragma clang loop unroll(disable)
               for (uint32_t j = g0; j < g1; ++j) {
+                const bool two_rows = has_row[1] && j % xparts == xpart;
                 uint32_t x[2];
 #pragma unroll
                 for (int mi = 0; mi < 2; ++mi) {
-                  const uint32_t m = (uint32_t)wave + 8u * mi;
+                  const uint32_t m = row[mi];
                   const uint32_t c0 = (m < ne0 && j < ne0) ? s_ld(cf0 + (m * K + j)) : 0u;
                   const uint32_t c1 = (m < ne1 && j < ne1) ? s_ld(cf1 + (m * K + j)) : 0u;
                   x[mi] = c0 | (c1 << 8);
@@ -1247,12 +1272,13 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
                 }
               }
             }
+            st.mark(19);
           }
           // (d)
 #pragma unroll
           for (int mi = 0; mi < 2; ++mi) {
-            const uint32_t m = (uint32_t)wave + 8u * mi;
-            if (m >= rt_rows) break;
+            const uint32_t m = row[mi];
+            if (!has_row[mi]) continue;
             const int p0 = m < ne0 ? (int)s_ld_u8(ep0, (int)m) : -1;
             const int p1 = m < ne1 ? (int)s_ld_u8(ep1, (int)m) : -1;
             if (p0 >= 0 && p0 == p1) {
@@ -1389,6 +1415,15 @@ __device__ __forceinline__ void restore_syn_body(const SynRestoreArgs &a) {
         if (RT ? (uint32_t)wave < rt_rows : perm_tile ? wave == 0 : wave < S::kM) {
           uint32_t Pl[16], W[16];
           syn_get_point(L, my_erased, Pl);
+          if constexpr (kDual) {
+            const int e1 = dual_tile ? (int)s_ld_u8(pl1->erased, wave) : my_erased;
+            if (e1 != my_erased) {  // (dual: half 1's row w is its own erased point)
+              uint32_t P1[16];
+              syn_get_point(L, e1, P1);
+#pragma unroll
+              for (int b = 0; b < 16; ++b) Pl[b] = __builtin_amdgcn_bitop3_b32(kRtH0, Pl[b], P1[b], 0xCA);
+            }
+          }
 #pragma unroll
           for (int b = 0; b < 16; ++b) W[b ^ 8] = Pl[b];
           transpose16x2(W, bm);  // self-inverse: back to the loaded word layout

@@ -311,11 +311,12 @@ def test_regenerate_batch_perm_noncodeword(gpu, k):
 
 
 def test_restore_batch_rt2_rows_noncodeword(gpu):
-    """RT2 (k = 32, every survivor below 2k, at most 8 erased points below k:
-    the PERM evaluations of P0 and the |E| x |E| products, ec_internal.hpp)
-    beside RT (9+ rows) in one batch call: random survivors, every trailer
-    kind, 1..12 rows, objects of one to three tiles and tiles whose halves
-    have different row counts, borrowed ids in any order."""
+    """RT2 (k = 32, every survivor below 2k, at most kRt2MaxRows = 12 erased
+    points below k: the PERM evaluations of P0 and the |E| x |E| products in
+    groups of eight, ec_internal.hpp; rows 9..12 spread over all waves) in one
+    batch call: random survivors, every trailer kind, 1..12 rows, objects of
+    one to three tiles and tiles whose halves have different row counts,
+    borrowed ids in any order."""
     import torch
     from vds_amd import chunk
     k = 32

@@ -302,6 +302,12 @@ inline bool id_set(uint32_t k, const uint16_t *nd, uint64_t *seen, uint32_t *max
 #define VDS_BATCH_DUAL 1
 #endif
 constexpr bool dual_enabled() { return VDS_BATCH_DUAL != 0; }
+// Tiles of unequal cost (the RT launch's, sorted by row count; a one-class
+// syndrome launch's dual tiles) interleaved over the XCDs' ranges (A/B: 0 =
+// in sorted order)
+#ifndef VDS_BATCH_RT_SPREAD
+#define VDS_BATCH_RT_SPREAD 1
+#endif
 
 // Host-side builder of one k_restore_syn batch launch, written straight into
 // a pinned parameter slot: objs (and the empty object), then tiles, then
@@ -582,7 +588,7 @@ struct SynBatchBuild {
     // the same mix of classes, whose tiles cost differently
     const uint64_t R = ntiles;
     auto pos = [&](uint64_t t) -> uint64_t {
-      if (ncls <= 1) return t;
+      if (ncls <= 1 && (ndual == 0 || !VDS_BATCH_RT_SPREAD)) return t;  // (dual tiles cost more: spread them too)
       const uint64_t r = t % 8;
       return r * (R / 8) + std::min<uint64_t>(r, R % 8) + t / 8;
     };
@@ -764,11 +770,29 @@ struct RtBatchBuild {
       return VDS_EC_EINVAL;
     }
     SynBatchTile *tiles = reinterpret_cast<SynBatchTile *>(slot->h + o_tiles);
+    // The tile count first (the mode boundary may leave a half empty), then
+    // the tiles at interleaved positions: each XCD's contiguous eighth of the
+    // launch (tile_range) gets every eighth tile of the sorted order, so every
+    // XCD has the same mix of row counts (in sorted order the heaviest tiles
+    // all landed on the last XCD, which then set the launch's length)
     uint64_t i = 0;
+    uint32_t cur = 0;
     for (const uint32_t o : order) {
-      if ((i & 1) && tiles[i / 2].mode != objs[o].rt.mode) ++i;  // (the other mode starts a new tile)
+      if ((i & 1) && cur != objs[o].rt.mode) ++i;
+      cur = objs[o].rt.mode;
+      i += obj_halves[o];
+    }
+    const uint64_t R = (i + 1) / 2;
+    auto pos = [&](uint64_t t) -> uint64_t {
+      if (!VDS_BATCH_RT_SPREAD) return t;
+      const uint64_t r = t % 8;
+      return r * (R / 8) + std::min<uint64_t>(r, R % 8) + t / 8;
+    };
+    i = 0;
+    for (const uint32_t o : order) {
+      if ((i & 1) && tiles[pos(i / 2)].mode != objs[o].rt.mode) ++i;  // (the other mode starts a new tile)
       for (uint32_t h = 0; h < obj_halves[o]; ++h, ++i) {
-        SynBatchTile &t = tiles[i / 2];
+        SynBatchTile &t = tiles[pos(i / 2)];
         if ((i & 1) == 0) t = SynBatchTile{{empty, empty}, {0, 0}, 0, 0, 0, objs[o].rt.mode};
         t.obj[i & 1] = o;
         t.stripe0[i & 1] = h * kHalfStripes;
@@ -776,7 +800,7 @@ struct RtBatchBuild {
         if (regen && h + 1 == obj_halves[o]) t.trailer |= 1u << (i & 1);
       }
     }
-    const uint64_t ntiles = (i + 1) / 2;
+    const uint64_t ntiles = R;
     hipError_t e = param_commit(slot, o_tiles + ntiles * sizeof(SynBatchTile), s);
     const SynBatchObj *dobjs = reinterpret_cast<const SynBatchObj *>(slot->d);
     if (e == hipSuccess) e = launch_rt_coefs(k, dobjs, nobj, s);

@@ -52,8 +52,12 @@ def test_batch_fuzz_vs_oracle(gpu):
     seconds = float(os.environ.get("VDS_FUZZ_SECONDS", "20"))
     seed0 = int(os.environ.get("VDS_FUZZ_SEED", "20261018"))
     t_end = time.monotonic() + seconds
+    t_note = time.monotonic() + 30
     it = 0
     while time.monotonic() < t_end:
+        if time.monotonic() > t_note:  # (a progress line: long soaks must not look hung)
+            print(f"batch fuzz: {it} calls", flush=True)
+            t_note += 30
         seed = seed0 + it
         it += 1
         rng = np.random.default_rng(seed)
